@@ -1,0 +1,478 @@
+/*
+ * msim_oracle.c — CPU ORACLE (test infrastructure only, never shipped, never measured as the product).
+ *
+ * A plain-C restatement of darosior/miningsimulation's per-run simulation loop, written to follow the
+ * reference line by line with EXPLICIT per-miner chains (exactly the data model of the reference), so
+ * that it can check the compact MI355X kernel.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.
+ *
+ * Reference (read-only, /root/reference):
+ *   xoroshiro128++.h:4-40   RNG (SplitMix64 seeding, rand64, exporand)
+ *   simulation.h:16-20      BLOCK_INTERVAL, PERC_MULTIPLIER, SELFISH_ARRIVAL
+ *   simulation.h:22-39      Block (+ Genesis, operator==)
+ *   simulation.h:41-202     Miner (FoundBlock, UnpublishedBlocks, NextArrival, SelfishBlocks,
+ *                            PublishedChain, MaybeReorg, MaybeSelfishReveal, NotifyBestChain)
+ *   simulation.h:205-221    NextBlockInterval, PickFinder
+ *   main.cpp:13-41          MinerStats
+ *   main.cpp:68-82          BestChain
+ *   main.cpp:99-112         EarliestArrival
+ *   main.cpp:128-192        RunSimulation
+ *
+ * Pinning: the reference cannot be built here unmodified (libstdc++ 11 lacks the C++20 chrono
+ * operator<< used at simulation.h:228 / main.cpp:225), so this restatement is pinned against
+ *   (1) the reference's own known-answer test, test.cpp:213-367 TestSelfishStrategy (tests/golden),
+ *   (2) reference outputs recorded in this container by the survey (RNG, interval,
+ *       picker KATs and two 64-run FNV hashes of per-run MinerStats),
+ *   (3) the README's published 32768-run averages (statistical).
+ *
+ * Arithmetic: glibc log1p / llround exactly as the reference calls them (compile with
+ * -ffp-contract=off; x86-64 baseline has no FMA, like the reference build line README.md:32).
+ */
+#include <assert.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "msim_oracle.h"
+
+/* simulation.h:16 BLOCK_INTERVAL = 600 s; used as nanoseconds (simulation.h:207). */
+#define OR_BLOCK_INTERVAL_NS 600000000000LL
+/* simulation.h:18 PERC_MULTIPLIER = UINT64_MAX / 100. */
+#define OR_PERC_MULTIPLIER (UINT64_MAX / 100u)
+/* simulation.h:20 SELFISH_ARRIVAL = milliseconds::max(). */
+#define OR_SELFISH_ARRIVAL INT64_MAX
+/* simulation.h:32 Genesis miner id = numeric_limits<unsigned>::max(). */
+#define OR_GENESIS_ID 0xFFFFFFFFu
+
+/* ---------------------------------------------------------------- RNG: xoroshiro128++.h:4-40 */
+
+/* xoroshiro128++.h:9-15 */
+static uint64_t or_splitmix64(uint64_t *seedval)
+{
+    uint64_t z = (*seedval += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+/* xoroshiro128++.h:23-24: m_s0 = SplitMix64(seedval), m_s1 = SplitMix64(seedval) (in order). */
+void oracle_rng_seed(oracle_rng *r, uint64_t seed)
+{
+    uint64_t s = seed;
+    r->s0 = or_splitmix64(&s);
+    r->s1 = or_splitmix64(&s);
+}
+
+static inline uint64_t or_rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+/* xoroshiro128++.h:26-34 */
+uint64_t oracle_rng_rand64(oracle_rng *r)
+{
+    uint64_t s0 = r->s0, s1 = r->s1;
+    const uint64_t result = or_rotl(s0 + s1, 17) + s0;
+    s1 ^= s0;
+    r->s0 = or_rotl(s0, 49) ^ s1 ^ (s1 << 21);
+    r->s1 = or_rotl(s1, 28);
+    return result;
+}
+
+/* xoroshiro128++.h:17-20 MakeExponentiallyDistributed, :36-39 exporand. */
+double oracle_exporand(oracle_rng *r, double mean)
+{
+    uint64_t u = oracle_rng_rand64(r);
+    double e = -log1p((double)(u >> 11) * -0x1.0p-53);
+    return mean * e;
+}
+
+/* simulation.h:205-210 NextBlockInterval: llround to ns, assert >= 0, duration_cast to ms. */
+int64_t oracle_next_block_interval(oracle_rng *r)
+{
+    const long long ns = llround(oracle_exporand(r, (double)OR_BLOCK_INTERVAL_NS));
+    assert(ns >= 0);
+    return (int64_t)(ns / 1000000LL);
+}
+
+/* simulation.h:213-221 PickFinder: first miner whose cumulative perc*PERC_MULTIPLIER exceeds a u64.
+ * Returns the miner INDEX, or -1 where the reference would hit its assert (simulation.h:220). */
+int oracle_pick_finder(const uint64_t *perc, int n, oracle_rng *r)
+{
+    uint64_t random = oracle_rng_rand64(r), i = 0;
+    for (int k = 0; k < n; ++k) {
+        i += perc[k] * OR_PERC_MULTIPLIER;
+        if (i > random) return k;
+    }
+    return -1;
+}
+
+/* ---------------------------------------------------------------- chains: simulation.h:22-202 */
+
+typedef struct {
+    uint32_t miner_id; /* simulation.h:24 */
+    int64_t arrival;   /* simulation.h:26 (ms) */
+} or_block;
+
+typedef struct {
+    uint32_t id;
+    uint64_t perc;
+    int64_t propagation;
+    or_block *chain;
+    size_t size, cap;
+    int stale_blocks;
+    int is_selfish;
+} or_miner;
+
+static void or_push(or_miner *m, uint32_t id, int64_t arrival)
+{
+    if (m->size == m->cap) {
+        m->cap = m->cap ? m->cap * 2 : 64;
+        m->chain = (or_block *)realloc(m->chain, m->cap * sizeof(or_block));
+        if (!m->chain) { fprintf(stderr, "oracle: out of memory\n"); abort(); }
+    }
+    m->chain[m->size].miner_id = id;
+    m->chain[m->size].arrival = arrival;
+    m->size++;
+}
+
+/* simulation.h:57-59: chain = {Genesis}, stale_blocks = 0. */
+static void or_miner_init(or_miner *m, const oracle_miner *d)
+{
+    memset(m, 0, sizeof(*m));
+    m->id = d->id;
+    m->perc = d->perc;
+    m->propagation = d->propagation_ms;
+    m->is_selfish = d->is_selfish;
+    or_push(m, OR_GENESIS_ID, 0);
+}
+
+/* simulation.h:105-115 SelfishBlocks: trailing count of SELFISH_ARRIVAL blocks. */
+static size_t or_selfish_blocks(const or_miner *m)
+{
+    size_t n = 0;
+    for (size_t i = m->size; i > 0; --i) {
+        if (m->chain[i - 1].arrival != OR_SELFISH_ARRIVAL) break;
+        ++n;
+    }
+    return n;
+}
+
+/* simulation.h:62-76 FoundBlock. */
+static void or_found_block(or_miner *m, int64_t block_time, size_t best_chain_size)
+{
+    if (m->is_selfish) {
+        const int is_race = or_selfish_blocks(m) == 1 && best_chain_size == m->size;
+        if (is_race) {
+            m->chain[m->size - 1].arrival = block_time + m->propagation;
+            or_push(m, m->id, block_time + m->propagation);
+        } else {
+            or_push(m, m->id, OR_SELFISH_ARRIVAL);
+        }
+    } else {
+        or_push(m, m->id, block_time + m->propagation);
+    }
+}
+
+/* simulation.h:79-89 UnpublishedBlocks. */
+static int or_unpublished_blocks(const or_miner *m, int64_t t)
+{
+    int n = 0;
+    for (size_t i = m->size; i > 0; --i) {
+        if (m->chain[i - 1].arrival <= t) break;
+        n++;
+    }
+    return n;
+}
+
+/* simulation.h:92-102 NextArrival. Returns 1 and sets *out if some block is in flight. */
+static int or_next_arrival(const or_miner *m, int64_t t, int64_t *out)
+{
+    int have = 0;
+    for (size_t i = m->size; i > 0; --i) {
+        if (m->chain[i - 1].arrival <= t) break;
+        *out = m->chain[i - 1].arrival;
+        have = 1;
+    }
+    return have;
+}
+
+/* The best chain is a span into one miner's vector (main.cpp:70): (owner index, length). */
+typedef struct {
+    int miner; /* -1: empty span */
+    size_t len;
+} or_span;
+
+static const or_block *or_span_data(const or_miner *ms, or_span s) { return ms[s.miner].chain; }
+
+/* simulation.h:124-142 MaybeReorg. */
+static void or_maybe_reorg(or_miner *m, const or_block *best, size_t best_len)
+{
+    if (best_len <= m->size) return;
+    for (size_t i = m->size; i > 0; --i) {
+        const or_block *b = &m->chain[m->size - 1];
+        if (b->miner_id == best[i - 1].miner_id && b->arrival == best[i - 1].arrival) break;
+        if (b->miner_id == m->id) m->stale_blocks++;
+        m->size--;
+    }
+    assert(best_len > m->size);
+    for (size_t i = m->size; i < best_len; ++i) or_push(m, best[i].miner_id, best[i].arrival);
+}
+
+/* simulation.h:149-174 MaybeSelfishReveal. */
+static void or_maybe_selfish_reveal(or_miner *m, size_t best_len, int64_t t)
+{
+    if (!m->is_selfish) return;
+    if (best_len > m->size) return;
+    const size_t selfish_count = or_selfish_blocks(m);
+    const size_t current_lead = m->size - best_len;
+    if (selfish_count > current_lead) {
+        size_t reveal_count = selfish_count - current_lead;
+        if (selfish_count > 1 && current_lead == 1) reveal_count = selfish_count;
+        for (size_t i = 0; i < reveal_count; ++i) {
+            size_t at = m->size - selfish_count + i;
+            assert(at < m->size); /* chain.at() bounds check */
+            m->chain[at].arrival = t + m->propagation;
+        }
+    }
+}
+
+/* simulation.h:177-180 NotifyBestChain. */
+static void or_notify(or_miner *m, const or_block *best, size_t best_len, int64_t t)
+{
+    or_maybe_selfish_reveal(m, best_len, t);
+    or_maybe_reorg(m, best, best_len);
+}
+
+/* main.cpp:68-82 BestChain (PublishedChain = simulation.h:118-121). */
+static or_span or_best_chain(const or_miner *ms, int n, int64_t t)
+{
+    or_span best = {-1, 0};
+    for (int k = 0; k < n; ++k) {
+        const size_t pub_len = ms[k].size - (size_t)or_unpublished_blocks(&ms[k], t);
+        const int more_work = pub_len > best.len;
+        const int first_seen = pub_len == best.len && pub_len != 0 &&
+                               ms[k].chain[pub_len - 1].arrival < or_span_data(ms, best)[best.len - 1].arrival;
+        if (more_work || first_seen) {
+            best.miner = k;
+            best.len = pub_len;
+        }
+    }
+    return best;
+}
+
+/* main.cpp:99-112 EarliestArrival. */
+static int or_earliest_arrival(const or_miner *ms, int n, int64_t t, int64_t *out)
+{
+    int have = 0;
+    int64_t ea = 0;
+    for (int k = 0; k < n; ++k) {
+        int64_t a;
+        if (or_next_arrival(&ms[k], t, &a)) {
+            if (have) ea = a < ea ? a : ea;
+            else ea = a;
+            have = 1;
+        }
+    }
+    if (have) *out = ea;
+    return have;
+}
+
+/* ---------------------------------------------------------------- RunSimulation: main.cpp:128-192 */
+
+int oracle_run(const oracle_miner *miners, int n, int64_t duration_ms, uint32_t seed_interval,
+               uint32_t seed_picker, oracle_run_stats *out, oracle_trace *trace)
+{
+    if (n <= 0) return ORACLE_EINVAL;
+    or_miner *ms = (or_miner *)calloc((size_t)n, sizeof(or_miner));
+    uint64_t *perc = (uint64_t *)calloc((size_t)n, sizeof(uint64_t));
+    for (int k = 0; k < n; ++k) {
+        or_miner_init(&ms[k], &miners[k]);
+        perc[k] = miners[k].perc;
+    }
+    int rc = 0;
+    /* main.cpp:131-134: the first rd() seeds the interval stream, the second the picker. */
+    oracle_rng block_interval, miner_picker;
+    oracle_rng_seed(&block_interval, seed_interval);
+    oracle_rng_seed(&miner_picker, seed_picker);
+
+    int64_t next_block_time = oracle_next_block_interval(&block_interval); /* main.cpp:138 */
+    size_t best_chain_size = 1;                                              /* main.cpp:149 */
+    uint64_t events = 0, finds = 0;
+    for (int64_t cur_time = 0; cur_time < duration_ms;) {
+        events++;
+        while (cur_time == next_block_time) { /* main.cpp:153-157 */
+            const int k = oracle_pick_finder(perc, n, &miner_picker);
+            if (k < 0) { rc = ORACLE_EPICK; goto done; }
+            or_found_block(&ms[k], next_block_time, best_chain_size);
+            next_block_time += oracle_next_block_interval(&block_interval);
+            finds++;
+        }
+        assert(cur_time < next_block_time); /* main.cpp:158 */
+
+        const or_span best = or_best_chain(ms, n, cur_time); /* main.cpp:164 */
+        const or_block *bd = or_span_data(ms, best);
+        for (int k = 0; k < n; ++k) or_notify(&ms[k], bd, best.len, cur_time); /* main.cpp:165-167 */
+        best_chain_size = best.len;                                              /* main.cpp:171 */
+
+        int64_t ea;                                  /* main.cpp:176-182 */
+        const int have = or_earliest_arrival(ms, n, cur_time, &ea);
+        cur_time = next_block_time;
+        if (have && ea < cur_time) cur_time = ea;
+    }
+    {
+        /* main.cpp:185-189 + MinerStats main.cpp:22-30. */
+        const or_span best = or_best_chain(ms, n, duration_ms);
+        const or_block *bd = or_span_data(ms, best);
+        for (int k = 0; k < n; ++k) {
+            long found = 0;
+            for (size_t i = 0; i < best.len; ++i)
+                if (bd[i].miner_id == ms[k].id) found++;
+            out[k].blocks_found = found;
+            out[k].stale_blocks = ms[k].stale_blocks;
+            out[k].blocks_share = found == 0 ? 0.0 : (double)found / (double)(best.len - 1);
+            out[k].stale_rate = found == 0 ? 0.0 : (double)ms[k].stale_blocks / (double)found;
+        }
+        if (trace) {
+            trace->events = events;
+            trace->finds = finds;
+            trace->best_len = best.len;
+        }
+    }
+done:
+    for (int k = 0; k < n; ++k) free(ms[k].chain);
+    free(ms);
+    free(perc);
+    return rc;
+}
+
+/* ---------------------------------------------------------------- batch driver (main.cpp:195-220) */
+
+typedef struct {
+    const oracle_miner *miners;
+    int n;
+    int64_t duration_ms;
+    uint64_t run_begin, n_runs;
+    uint32_t seed_base;
+    int nthreads, tid;
+    oracle_run_stats *per_run; /* n_runs * n, may be NULL */
+    int rc;
+} or_job;
+
+static void *or_worker(void *arg)
+{
+    or_job *j = (or_job *)arg;
+    oracle_run_stats *tmp = (oracle_run_stats *)calloc((size_t)j->n, sizeof(oracle_run_stats));
+    for (uint64_t r = (uint64_t)j->tid; r < j->n_runs; r += (uint64_t)j->nthreads) {
+        const uint64_t run = j->run_begin + r;
+        /* Seed convention: run r uses rd()-equivalents (base+2r, base+2r+1) mod 2^32. */
+        const uint32_t si = (uint32_t)(j->seed_base + 2u * run);
+        const uint32_t sp = (uint32_t)(j->seed_base + 2u * run + 1u);
+        oracle_run_stats *o = j->per_run ? &j->per_run[r * (uint64_t)j->n] : tmp;
+        int rc = oracle_run(j->miners, j->n, j->duration_ms, si, sp, o, NULL);
+        if (rc) { j->rc = rc; break; }
+    }
+    free(tmp);
+    return NULL;
+}
+
+int oracle_run_batch(const oracle_miner *miners, int n, int64_t duration_ms, uint64_t run_begin,
+                     uint64_t n_runs, uint32_t seed_base, int nthreads, oracle_run_stats *per_run,
+                     oracle_stats_sum *sums)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (!per_run && sums) {
+        /* sums need per-run values in run order; allocate internally. */
+        per_run = (oracle_run_stats *)calloc(n_runs * (uint64_t)n, sizeof(oracle_run_stats));
+        int rc = oracle_run_batch(miners, n, duration_ms, run_begin, n_runs, seed_base, nthreads, per_run, sums);
+        free(per_run);
+        return rc;
+    }
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    or_job *jobs = (or_job *)calloc((size_t)nthreads, sizeof(or_job));
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (or_job){miners, n, duration_ms, run_begin, n_runs, seed_base, nthreads, t, per_run, 0};
+        pthread_create(&th[t], NULL, or_worker, &jobs[t]);
+    }
+    int rc = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+    }
+    free(th);
+    free(jobs);
+    if (rc) return rc;
+    if (sums && per_run) {
+        /* main.cpp:211-217: stats_total[j] += stats[j], in run order (MinerStats::operator+= 34-40). */
+        for (int k = 0; k < n; ++k) {
+            sums[k].blocks_found = 0;
+            sums[k].blocks_share = 0.0;
+            sums[k].stale_rate = 0.0;
+        }
+        for (uint64_t r = 0; r < n_runs; ++r)
+            for (int k = 0; k < n; ++k) {
+                const oracle_run_stats *o = &per_run[r * (uint64_t)n + (uint64_t)k];
+                sums[k].blocks_found += o->blocks_found;
+                sums[k].blocks_share += o->blocks_share;
+                sums[k].stale_rate += o->stale_rate;
+            }
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- explicit-chain state machine API
+ * (used to replay test.cpp:213-367 TestSelfishStrategy against this restatement). */
+
+struct oracle_miner_state {
+    or_miner m;
+};
+
+oracle_miner_state *oracle_state_new(const oracle_miner *d)
+{
+    oracle_miner_state *s = (oracle_miner_state *)calloc(1, sizeof(*s));
+    or_miner_init(&s->m, d);
+    return s;
+}
+
+void oracle_state_free(oracle_miner_state *s)
+{
+    if (!s) return;
+    free(s->m.chain);
+    free(s);
+}
+
+void oracle_state_set_chain(oracle_miner_state *s, const uint32_t *ids, const int64_t *arrivals, size_t len)
+{
+    s->m.size = 0;
+    for (size_t i = 0; i < len; ++i) or_push(&s->m, ids[i], arrivals[i]);
+}
+
+size_t oracle_state_get_chain(const oracle_miner_state *s, uint32_t *ids, int64_t *arrivals, size_t cap)
+{
+    for (size_t i = 0; i < s->m.size && i < cap; ++i) {
+        ids[i] = s->m.chain[i].miner_id;
+        arrivals[i] = s->m.chain[i].arrival;
+    }
+    return s->m.size;
+}
+
+int oracle_state_stale(const oracle_miner_state *s) { return s->m.stale_blocks; }
+
+void oracle_state_found_block(oracle_miner_state *s, int64_t block_time, size_t best_chain_size)
+{
+    or_found_block(&s->m, block_time, best_chain_size);
+}
+
+void oracle_state_notify(oracle_miner_state *s, const uint32_t *ids, const int64_t *arrivals, size_t len, int64_t t)
+{
+    or_block *b = (or_block *)malloc((len ? len : 1) * sizeof(or_block));
+    for (size_t i = 0; i < len; ++i) {
+        b[i].miner_id = ids[i];
+        b[i].arrival = arrivals[i];
+    }
+    or_notify(&s->m, b, len, t);
+    free(b);
+}
+
+int64_t oracle_selfish_arrival(void) { return OR_SELFISH_ARRIVAL; }
+uint32_t oracle_genesis_id(void) { return OR_GENESIS_ID; }
