@@ -1,0 +1,181 @@
+"""Throughput benchmark: simulated run-years/s of darosior/miningsimulation's per-run loop on MI355X.
+
+One step = one batch of `--runs` (default 32768 = SIM_RUNS, main.cpp:10) independent runs of
+RunSimulation(months{12}) per GPU on BASELINE.json configs[1] (9-miner 2025 network, 100 ms propagation),
+followed by the single exchange step of the path: an RCCL all-reduce of the per-miner integer sums.
+Weak scaling: per-GPU work is fixed; each step and rank takes a fresh, disjoint run range (fresh seeds).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--runs 32768]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL over xGMI)
+
+Rank 0 prints ONE JSON line (driver contract) with a live VALU roofline (HIP events around every launch
+on the launch stream) and, at N=1, the CPU baseline: the oracle (explicit-chain C port of the reference
+loop, oracle/msim_oracle.c) timed on a bounded sample on the host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# MI355X VALU peak (MI355X_MICROARCH.md: 256 CUs, 4 SIMD-32 per CU, 2.4 GHz): 256*4*32*2.4e9 lane-ops/s.
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL = 52594.92
+
+
+def w_blk(m: int) -> int:
+    """SURVEY §8(d) fixed accounting convention: algorithmic VALU lane-ops per simulated block."""
+    import math
+
+    return 140 + 4 * math.ceil(math.log2(max(m, 2)))
+
+
+def cpu_baseline(preset: str, sample_runs: int, threads: int) -> dict:
+    from oracle import pyoracle
+
+    pyoracle.build()
+    out = subprocess.run([pyoracle.CLI, "time", preset, str(sample_runs), str(threads)], capture_output=True,
+                         text=True, check=True)
+    rec = json.loads(out.stdout.splitlines()[0])
+    return {
+        "value": round(rec["run_years_per_s"], 2),
+        "unit": "run-years/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sample_runs} runs x 365.2425 d of preset {preset} (oracle/msim_oracle.c, explicit chains as "
+                  f"in the reference, {threads} pthreads), {rec['seconds']:.1f} s wall",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "default"])
+    ap.add_argument("--runs", type=int, default=32768, help="runs per GPU per step")
+    ap.add_argument("--seed-base", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from miningsimulation_amd import PRESETS, Simulation
+
+    miners = PRESETS[args.config]()
+    m = len(miners)
+    sim = Simulation(miners)
+    n = args.runs
+    dev = torch.device("cuda", local)
+    ws = torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev)
+    sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+    total = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+    status = torch.zeros(2, dtype=torch.int32, device=dev)
+    fails = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(i: int, ev=None):
+        begin = (i * world + rank) * n  # disjoint run ranges per step and rank -> fresh seeds
+        if ev is not None:
+            ev[0].record(stream)
+        sim.launch(n, begin, args.seed_base, sums, ws, status, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        fails.add_(status[1:2].to(torch.int64))
+        if world > 1:
+            dist.all_reduce(sums)  # the path's only exchange: per-miner integer sums (RCCL over xGMI)
+        total.add_(sums)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    total.zero_()
+    fails.zero_()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(fails)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    if int(fails.item()) != 0:
+        raise SystemExit(f"{int(fails.item())} runs exceeded the compact state capacity")
+
+    runs_total = args.steps * n * world
+    value = runs_total / elapsed
+    per_gpu_kernel_rate = n / (kern_ms / 1e3)  # run-years/s of one launch on one GPU
+    achieved = per_gpu_kernel_rate * BLOCKS_PER_RUN_YEAR * w_blk(m)  # algorithmic lane-ops/s per GPU
+    # sanity: aggregate share of miner 0 (integer sums, exact across ranks)
+    tot = total.cpu().tolist()
+    share0 = (tot[0][2] + tot[0][3] * 2.0**-32) / (runs_total) * 100
+
+    if rank == 0:
+        line = {
+            "metric": "simulated run-years/sec (whole node) at 1/2/4/8 MI355X; % of VALU peak",
+            "value": round(value, 1),
+            "unit": "run-years/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64+fp64",
+            "data": "synthetic (seeded runs; run r uses rd()-equivalents (base+2r, base+2r+1))",
+            "config": {
+                "workload": f"{args.config}: BASELINE configs[1]" if args.config == "c2" else args.config,
+                "network": [[mm.id, mm.perc, mm.propagation_ms, int(mm.is_selfish)] for mm in miners],
+                "runs_per_gpu_per_step": n,
+                "duration": "months{12} = 31556952000 ms",
+                "parallelism": f"runs sharded over {world} GPU(s), RCCL all-reduce of per-miner integer sums",
+                "miner0_share_pct": round(share0, 5),
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved / 1e12, 4),
+                "peak": round(VALU_PEAK_LANE_OPS / 1e12, 2),
+                "unit": "T lane-op/s",
+                "frac": round(achieved / VALU_PEAK_LANE_OPS, 5),
+                "traffic": None,
+                "kernel_ms": round(kern_ms, 4),
+                "accounting": f"SURVEY 8(d): W_blk({m}) = {w_blk(m)} lane-ops/block x 52594.92 blocks/run-year",
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = max(1, min(16, os.cpu_count() or 1))
+            sample = args.cpu_sample_runs or threads * 96
+            line["cpu_baseline"] = cpu_baseline(args.config, sample, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

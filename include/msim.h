@@ -1,0 +1,116 @@
+/*
+ * msim.h — C ABI of libmsim, the MI355X (gfx950) engine for darosior/miningsimulation's per-run
+ * simulation loop. Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ *
+ * What each entry point replaces in the reference (/root/reference):
+ *   msim_miner            <- Miner(unsigned id, uint64_t perc, milliseconds prop, bool selfish)
+ *                            simulation.h:57-59, as built by SetupMiners() main.cpp:44-65
+ *   msim_config_create    <- SetupMiners() + SIM_DURATION (main.cpp:7, 44-65); validates what the
+ *                            reference only asserts (simulation.h:220: percentages must sum to 100)
+ *   msim_run              <- the std::async batch loop of main() (main.cpp:195-220): SIM_RUNS calls of
+ *                            RunSimulation(SIM_DURATION, miners) (main.cpp:128-192, :209) and the
+ *                            stats_total[j] += stats[j] aggregation (main.cpp:211-217)
+ *   msim_stats            <- MinerStats {long blocks_found; double blocks_share; double stale_rate;}
+ *                            (main.cpp:13-20), same field order and types
+ *   msim_launch           <- device-resident form of msim_run for hosts that own streams and an
+ *                            RCCL communicator (multi-GPU: shard runs, all-reduce msim_sums)
+ * Seeds: RunSimulation draws two 32-bit std::random_device values (main.cpp:131-134); run r of a
+ * launch uses (seed_base + 2r, seed_base + 2r + 1) mod 2^32 for (block_interval, miner_picker).
+ */
+#ifndef MSIM_H
+#define MSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSIM_OK 0
+#define MSIM_E_INVALID (-1)  /* bad argument (null pointer, n == 0, negative duration/propagation) */
+#define MSIM_E_WEIGHTS (-2)  /* percentages above 100 in total (reference: u64 wrap / assert) */
+#define MSIM_E_SELFISH (-3)  /* more than one selfish miner (device path supports at most one) */
+#define MSIM_E_MINERS (-4)   /* more than MSIM_MAX_MINERS miners, or duplicate miner ids */
+#define MSIM_E_HIP (-5)      /* HIP runtime error (no device, launch failure, out of memory) */
+#define MSIM_E_CAPACITY (-6) /* a run exceeded the compact state's capacity even on the retry kernel */
+#define MSIM_E_PICK (-7)     /* PickFinder fell through (simulation.h:220 assert): percentages < 100 */
+
+#define MSIM_MAX_MINERS 15
+
+typedef struct msim_miner {
+    uint32_t id;            /* Miner::id (simulation.h:43) */
+    uint64_t perc;          /* Miner::perc, integer percent of network hashrate (simulation.h:45) */
+    int64_t propagation_ms; /* Miner::propagation (simulation.h:47) */
+    uint8_t is_selfish;     /* Miner::is_selfish (simulation.h:55) */
+} msim_miner;
+
+typedef struct msim_config msim_config;
+
+/* Per-miner aggregate over runs, bit layout of MinerStats (main.cpp:13-20). */
+typedef struct msim_stats {
+    int64_t blocks_found;
+    double blocks_share;
+    double stale_rate;
+} msim_stats;
+
+/* Order-independent device sums per miner (integers, so 1/2/4/8-GPU all-reduces are bit-identical).
+ * share and stale_rate are summed as Q32.32 fixed point split into 32-bit limbs:
+ *   sum(share) = share_hi + share_lo * 2^-32 (exact integer sums of per-run round(share * 2^32)). */
+typedef struct msim_sums {
+    int64_t blocks_found;
+    int64_t stale_blocks;
+    uint64_t share_hi, share_lo;
+    uint64_t rate_hi, rate_lo;
+} msim_sums;
+
+/* Per-run, per-miner integer counters (the bit-exact parity surface). */
+typedef struct msim_run_record {
+    uint32_t found; /* blocks of this miner in the final best chain (main.cpp:24-26) */
+    uint32_t stale; /* Miner::stale_blocks at the end of the run (simulation.h:133) */
+} msim_run_record;
+
+int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms, msim_config **out);
+void msim_config_destroy(msim_config *cfg);
+uint32_t msim_config_miner_count(const msim_config *cfg);
+
+/* Run runs [run_begin, run_begin + n_runs) on HIP device `device`.
+ * out_sums: M entries (like stats_total, main.cpp:199); with opt_per_run given, the share/stale_rate
+ *           doubles are summed on the host in run order exactly as main.cpp:211-217 does; otherwise
+ *           they come from the fixed-point device sums (relative error < 1e-9).
+ * opt_per_run: n_runs * M records or NULL; opt_best_height: n_runs entries (|best chain| - 1) or NULL.
+ * opt_sums: M fixed-point msim_sums or NULL. */
+int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, int device,
+             msim_stats *out_sums, msim_sums *opt_sums, msim_run_record *opt_per_run, uint32_t *opt_best_height);
+
+/* Device-resident launch on the current HIP device and the given hipStream_t (NULL = default).
+ * d_sums: M msim_sums in device memory (overwritten). d_per_run / d_best_height: device buffers or NULL.
+ * d_status: 2 uint32_t in device memory: [0] = runs that needed the retry kernel, [1] = runs that
+ * failed even there (each failed run contributes nothing to d_sums).
+ * d_workspace / workspace_bytes: scratch from msim_workspace_bytes(); the call does no allocation
+ * and no synchronisation, so it can be captured into a hipGraph. */
+size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs);
+int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, void *d_sums,
+                void *d_per_run, void *d_best_height, void *d_status, void *d_workspace, size_t workspace_bytes,
+                void *stream);
+
+/* Device draw primitives (bit-exact with the reference's host libm; test and sampler surface):
+ *   msim_device_log1p     glibc log1p on the reference's domain (xoroshiro128++.h:19)
+ *   msim_device_intervals NextBlockInterval of given uniform u64 draws, in ms (simulation.h:205-210)
+ *   msim_device_picks     PickFinder index of given uniform u64 draws (simulation.h:213-221)
+ * All pointers are device memory; launches go to `stream` (hipStream_t, NULL = default). */
+int msim_device_log1p(const double *d_x, double *d_out, uint64_t n, void *stream);
+int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t n, void *stream);
+int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t *d_out_index, uint64_t n,
+                      void *stream);
+
+/* Convert fixed-point sums to MinerStats-style doubles. */
+void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out);
+
+const char *msim_strerror(int code);
+const char *msim_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSIM_H */

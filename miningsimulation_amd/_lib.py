@@ -1,0 +1,121 @@
+"""ctypes binding of libmsim.so (include/msim.h).
+
+The library is GPU-only: there is no CPU fallback anywhere in the product path. Importing this module
+without a built ``libmsim.so`` raises immediately; calling into it without a HIP device returns
+MSIM_E_HIP, which the wrappers turn into :class:`MsimError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MSIM_LIB", os.path.join(_HERE, "libmsim.so"))
+
+MSIM_OK = 0
+MSIM_E_INVALID = -1
+MSIM_E_WEIGHTS = -2
+MSIM_E_SELFISH = -3
+MSIM_E_MINERS = -4
+MSIM_E_HIP = -5
+MSIM_E_CAPACITY = -6
+MSIM_E_PICK = -7
+MSIM_MAX_MINERS = 15
+
+# Every symbol include/msim.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "msim_config_create",
+    "msim_config_destroy",
+    "msim_config_miner_count",
+    "msim_run",
+    "msim_workspace_bytes",
+    "msim_launch",
+    "msim_device_log1p",
+    "msim_device_intervals",
+    "msim_device_picks",
+    "msim_sums_to_stats",
+    "msim_strerror",
+    "msim_version",
+)
+
+
+class MsimMiner(ctypes.Structure):
+    _fields_ = [
+        ("id", ctypes.c_uint32),
+        ("perc", ctypes.c_uint64),
+        ("propagation_ms", ctypes.c_int64),
+        ("is_selfish", ctypes.c_uint8),
+    ]
+
+
+class MsimStats(ctypes.Structure):
+    _fields_ = [("blocks_found", ctypes.c_int64), ("blocks_share", ctypes.c_double), ("stale_rate", ctypes.c_double)]
+
+
+class MsimSums(ctypes.Structure):
+    _fields_ = [
+        ("blocks_found", ctypes.c_int64),
+        ("stale_blocks", ctypes.c_int64),
+        ("share_hi", ctypes.c_uint64),
+        ("share_lo", ctypes.c_uint64),
+        ("rate_hi", ctypes.c_uint64),
+        ("rate_lo", ctypes.c_uint64),
+    ]
+
+
+class MsimRunRecord(ctypes.Structure):
+    _fields_ = [("found", ctypes.c_uint32), ("stale", ctypes.c_uint32)]
+
+
+class MsimError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {strerror(code)} ({code})" if what else f"{strerror(code)} ({code})")
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libmsim.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the simulation path is HIP-only; there is no CPU fallback)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i64, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64, ctypes.c_size_t
+    lib.msim_config_create.argtypes = [ctypes.POINTER(MsimMiner), u32, i64, ctypes.POINTER(vp)]
+    lib.msim_config_create.restype = ctypes.c_int
+    lib.msim_config_destroy.argtypes = [vp]
+    lib.msim_config_destroy.restype = None
+    lib.msim_config_miner_count.argtypes = [vp]
+    lib.msim_config_miner_count.restype = u32
+    lib.msim_run.argtypes = [vp, u64, u64, u32, ctypes.c_int, ctypes.POINTER(MsimStats), ctypes.POINTER(MsimSums),
+                             ctypes.POINTER(MsimRunRecord), ctypes.POINTER(u32)]
+    lib.msim_run.restype = ctypes.c_int
+    lib.msim_workspace_bytes.argtypes = [vp, u64]
+    lib.msim_workspace_bytes.restype = sz
+    lib.msim_launch.argtypes = [vp, u64, u64, u32, vp, vp, vp, vp, vp, sz, vp]
+    lib.msim_launch.restype = ctypes.c_int
+    lib.msim_device_log1p.argtypes = [vp, vp, u64, vp]
+    lib.msim_device_log1p.restype = ctypes.c_int
+    lib.msim_device_intervals.argtypes = [vp, vp, u64, vp]
+    lib.msim_device_intervals.restype = ctypes.c_int
+    lib.msim_device_picks.argtypes = [vp, vp, vp, u64, vp]
+    lib.msim_device_picks.restype = ctypes.c_int
+    lib.msim_sums_to_stats.argtypes = [ctypes.POINTER(MsimSums), u32, ctypes.POINTER(MsimStats)]
+    lib.msim_sums_to_stats.restype = None
+    lib.msim_strerror.argtypes = [ctypes.c_int]
+    lib.msim_strerror.restype = ctypes.c_char_p
+    lib.msim_version.argtypes = []
+    lib.msim_version.restype = ctypes.c_char_p
+    return lib
+
+
+lib = _load()
+
+
+def strerror(code: int) -> str:
+    return lib.msim_strerror(code).decode()
+
+
+def check(code: int, what: str = "") -> None:
+    if code != MSIM_OK:
+        raise MsimError(code, what)

@@ -1,0 +1,245 @@
+// msim_api.hip — the C ABI declared in include/msim.h.
+//
+// msim_run replaces main()'s batch loop (/root/reference/main.cpp:195-220): the reference starts one
+// std::async thread per RunSimulation call, in barrier-synchronised batches of hardware_concurrency(),
+// and sums MinerStats in run order on the main thread. Here one launch runs a whole shard of runs,
+// one run per lane, and the per-miner sums are reduced on the device in integers.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/msim.h"
+#include "msim_kernels.h"
+
+struct msim_config {
+    msim::SimParams p;
+    uint32_t n;
+    uint32_t ids[MSIM_MAX_MINERS];
+};
+
+namespace {
+
+uint32_t err_cap_for(uint64_t n)
+{
+    uint64_t c = n < 65536 ? n : 65536;
+    if (c < 256) c = 256;
+    return (uint32_t)((c + 255) / 256 * 256);
+}
+
+struct WsLayout {
+    size_t partials_off, counts_off, list_off, total;
+    uint32_t err_cap;
+};
+
+WsLayout ws_layout(uint32_t m, uint64_t n)
+{
+    WsLayout l;
+    l.err_cap = err_cap_for(n);
+    l.partials_off = 0;
+    l.counts_off = msim::partials_words(m, (uint32_t)n, l.err_cap) * sizeof(uint64_t);
+    l.list_off = l.counts_off + 2 * sizeof(uint32_t);
+    l.total = l.list_off + (size_t)l.err_cap * sizeof(uint32_t);
+    l.total = (l.total + 255) / 256 * 256;
+    return l;
+}
+
+constexpr uint64_t MAX_LAUNCH_RUNS = 1ull << 26;
+
+}  // namespace
+
+extern "C" {
+
+int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms, msim_config **out)
+{
+    if (!miners || !out || n == 0 || duration_ms < 0) return MSIM_E_INVALID;
+    if (n > MSIM_MAX_MINERS) return MSIM_E_MINERS;
+    uint64_t perc[MSIM_MAX_MINERS];
+    int64_t prop[MSIM_MAX_MINERS];
+    uint8_t self[MSIM_MAX_MINERS];
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        for (uint32_t j = 0; j < k; ++j)
+            if (miners[j].id == miners[k].id) return MSIM_E_MINERS;
+        perc[k] = miners[k].perc;
+        prop[k] = miners[k].propagation_ms;
+        self[k] = miners[k].is_selfish ? 1 : 0;
+        if (prop[k] < 0) return MSIM_E_INVALID;
+        if (perc[k] > 100) return MSIM_E_WEIGHTS;
+        total += perc[k];
+    }
+    // "Must add up to 1" (main.cpp:43); anything else makes PickFinder assert (simulation.h:220).
+    if (total != 100) return MSIM_E_WEIGHTS;
+    msim_config *c = (msim_config *)calloc(1, sizeof(msim_config));
+    if (!c) return MSIM_E_INVALID;
+    const int rc = msim::make_params(perc, prop, self, (int)n, duration_ms, &c->p);
+    if (rc) {
+        free(c);
+        return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
+    }
+    c->n = n;
+    for (uint32_t k = 0; k < n; ++k) c->ids[k] = miners[k].id;
+    *out = c;
+    return MSIM_OK;
+}
+
+void msim_config_destroy(msim_config *cfg) { free(cfg); }
+
+uint32_t msim_config_miner_count(const msim_config *cfg) { return cfg ? cfg->n : 0; }
+
+size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
+{
+    if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
+    return ws_layout(cfg->n, n_runs).total;
+}
+
+int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, void *d_sums,
+                void *d_per_run, void *d_best_height, void *d_status, void *d_workspace, size_t workspace_bytes,
+                void *stream)
+{
+    if (!cfg || !d_sums || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    const WsLayout l = ws_layout(cfg->n, n_runs);
+    if (workspace_bytes < l.total) return MSIM_E_INVALID;
+    char *ws = (char *)d_workspace;
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t *counts = (uint32_t *)(ws + l.counts_off);
+    if (hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return MSIM_E_HIP;
+    msim::LaunchArgs a;
+    a.p = cfg->p;
+    a.run_begin = run_begin;
+    a.n = (uint32_t)n_runs;
+    a.seed_base = seed_base;
+    a.partials = (uint64_t *)(ws + l.partials_off);
+    a.sums = (uint64_t *)d_sums;
+    a.records = (uint32_t *)d_per_run;
+    a.best_h = (uint32_t *)d_best_height;
+    a.err_count = counts;
+    a.fail_count = counts + 1;
+    a.err_list = (uint32_t *)(ws + l.list_off);
+    a.err_cap = l.err_cap;
+    a.status = (uint32_t *)d_status;
+    a.stream = s;
+    return msim::launch_runs(a) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+}
+
+int msim_device_log1p(const double *d_x, double *d_out, uint64_t n, void *stream)
+{
+    if (!d_x || !d_out) return MSIM_E_INVALID;
+    return msim::launch_log1p(d_x, d_out, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+}
+
+int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t n, void *stream)
+{
+    if (!d_uniform || !d_out_ms) return MSIM_E_INVALID;
+    return msim::launch_intervals(d_uniform, d_out_ms, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+}
+
+int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t *d_out_index, uint64_t n, void *stream)
+{
+    if (!cfg || !d_uniform || !d_out_index) return MSIM_E_INVALID;
+    return msim::launch_picks(cfg->p, d_uniform, d_out_index, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+}
+
+void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out)
+{
+    for (uint32_t k = 0; k < n; ++k) {
+        out[k].blocks_found = sums[k].blocks_found;
+        out[k].blocks_share = (double)sums[k].share_hi + (double)sums[k].share_lo * 0x1.0p-32;
+        out[k].stale_rate = (double)sums[k].rate_hi + (double)sums[k].rate_lo * 0x1.0p-32;
+    }
+}
+
+int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, int device,
+             msim_stats *out_sums, msim_sums *opt_sums, msim_run_record *opt_per_run, uint32_t *opt_best_height)
+{
+    if (!cfg || !out_sums || n_runs == 0) return MSIM_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return MSIM_E_HIP;
+    const uint32_t m = cfg->n;
+    const uint64_t chunk = n_runs < MAX_LAUNCH_RUNS ? n_runs : MAX_LAUNCH_RUNS;
+    const size_t wsb = ws_layout(m, chunk).total;
+    void *ws = nullptr, *sums = nullptr, *status = nullptr, *rec = nullptr, *bh = nullptr;
+    const bool want_rec = opt_per_run != nullptr;
+    const bool want_bh = want_rec || opt_best_height != nullptr;
+    int rc = MSIM_OK;
+    std::vector<uint32_t> bh_host;
+    if (want_rec && !opt_best_height) bh_host.resize(n_runs);
+    uint32_t *bh_out = opt_best_height ? opt_best_height : (want_rec ? bh_host.data() : nullptr);
+    std::vector<uint64_t> acc(6 * (size_t)m, 0), part(6 * (size_t)m);
+    uint32_t st[2];
+    hipStream_t s = nullptr;
+    if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&sums, 6 * sizeof(uint64_t) * m) != hipSuccess ||
+        hipMalloc(&status, 2 * sizeof(uint32_t)) != hipSuccess ||
+        (want_rec && hipMalloc(&rec, chunk * m * sizeof(msim_run_record)) != hipSuccess) ||
+        (want_bh && hipMalloc(&bh, chunk * sizeof(uint32_t)) != hipSuccess) || hipStreamCreate(&s) != hipSuccess) {
+        rc = MSIM_E_HIP;
+        goto out;
+    }
+    for (uint64_t off = 0; off < n_runs && rc == MSIM_OK; off += chunk) {
+        const uint64_t cn = (n_runs - off) < chunk ? (n_runs - off) : chunk;
+        rc = msim_launch(cfg, run_begin + off, cn, seed_base, sums, rec, bh, status, ws, wsb, s);
+        if (rc) break;
+        if (hipMemcpyAsync(part.data(), sums, part.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(st, status, sizeof(st), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            (want_rec && hipMemcpyAsync(opt_per_run + off * m, rec, cn * m * sizeof(msim_run_record),
+                                        hipMemcpyDeviceToHost, s) != hipSuccess) ||
+            (want_bh && hipMemcpyAsync(bh_out + off, bh, cn * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            rc = MSIM_E_HIP;
+            break;
+        }
+        if (st[1] != 0) {
+            rc = MSIM_E_CAPACITY;
+            break;
+        }
+        for (size_t i = 0; i < acc.size(); ++i) acc[i] += part[i];
+    }
+    if (rc == MSIM_OK) {
+        msim_sums *fs = (msim_sums *)acc.data();
+        if (opt_sums) memcpy(opt_sums, fs, sizeof(msim_sums) * m);
+        msim_sums_to_stats(fs, m, out_sums);
+        if (want_rec) {
+            // Exact reference aggregation: per-run MinerStats (main.cpp:22-30) summed in run order
+            // (main.cpp:211-217, MinerStats::operator+= 34-40).
+            for (uint32_t k = 0; k < m; ++k) {
+                out_sums[k].blocks_share = 0.0;
+                out_sums[k].stale_rate = 0.0;
+            }
+            for (uint64_t r = 0; r < n_runs; ++r)
+                for (uint32_t k = 0; k < m; ++k) {
+                    const msim_run_record &x = opt_per_run[r * m + k];
+                    const double share = x.found == 0 ? 0.0 : (double)x.found / (double)bh_out[r];
+                    const double rate = x.found == 0 ? 0.0 : (double)x.stale / (double)x.found;
+                    out_sums[k].blocks_share += share;
+                    out_sums[k].stale_rate += rate;
+                }
+        }
+    }
+out:
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipFree(ws);
+    (void)hipFree(sums);
+    (void)hipFree(status);
+    (void)hipFree(rec);
+    (void)hipFree(bh);
+    return rc;
+}
+
+const char *msim_strerror(int code)
+{
+    switch (code) {
+    case MSIM_OK: return "ok";
+    case MSIM_E_INVALID: return "invalid argument";
+    case MSIM_E_WEIGHTS: return "miner percentages must be integers in [0,100] adding up to 100";
+    case MSIM_E_SELFISH: return "at most one selfish miner is supported on the device path";
+    case MSIM_E_MINERS: return "too many miners (max 15) or duplicate miner ids";
+    case MSIM_E_HIP: return "HIP runtime error";
+    case MSIM_E_CAPACITY: return "a run exceeded the compact state capacity";
+    case MSIM_E_PICK: return "PickFinder fell through its table";
+    default: return "unknown error";
+    }
+}
+
+const char *msim_version(void) { return "msim 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,96 @@
+// msim_common.hip — finalize kernel and the runtime miner-count dispatch (compiled once).
+#include <hip/hip_runtime.h>
+
+#include "msim_kernels.h"
+
+namespace msim {
+
+__global__ void msim_finalize(const uint64_t *__restrict__ partials, uint32_t nparts, uint32_t nvals,
+                              uint64_t *__restrict__ out, const uint32_t *__restrict__ retry_count,
+                              const uint32_t *__restrict__ fail_count, const uint32_t retry_cap,
+                              uint32_t *__restrict__ status)
+{
+    for (uint32_t i = threadIdx.x; i < nvals; i += blockDim.x) {
+        uint64_t s = 0;
+        for (uint32_t b = 0; b < nparts; ++b) s += partials[(size_t)b * nvals + i];
+        out[i] = s;
+    }
+    if (threadIdx.x == 0 && status) {
+        const uint32_t rc = *retry_count;
+        status[0] = rc;
+        status[1] = *fail_count + (rc > retry_cap ? rc - retry_cap : 0u);
+    }
+}
+
+__global__ void msim_log1p_kernel(const double *__restrict__ x, double *__restrict__ out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = glibc_log1p(x[i]);
+}
+
+__global__ void msim_interval_kernel(const uint64_t *__restrict__ u, int64_t *__restrict__ out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = interval_ms_of(u[i]);
+}
+
+__global__ void msim_pick_kernel(const SimParams p, const uint64_t *__restrict__ u, int32_t *__restrict__ out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    // PickFinder's running sum (simulation.h:216-218) over the runtime miner count.
+    int k = 0;
+    for (int j = 0; j < p.m; ++j) k += (p.thresh[j] <= u[i]) ? 1 : 0;
+    out[i] = k < p.m ? k : -1;
+}
+
+hipError_t launch_log1p(const double *x, double *out, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(msim_log1p_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_intervals(const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(msim_interval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_picks(const SimParams &p, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(msim_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, u, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const uint64_t *partials, uint32_t nparts, uint32_t nvals, uint64_t *out,
+                           const uint32_t *retry_count, const uint32_t *fail_count, uint32_t retry_cap,
+                           uint32_t *status, hipStream_t stream)
+{
+    hipLaunchKernelGGL(msim_finalize, dim3(1), dim3(TPB), 0, stream, partials, nparts, nvals, out, retry_count,
+                       fail_count, retry_cap, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_runs(const LaunchArgs &a)
+{
+    switch (a.p.m) {
+#define CASE(MM) \
+    case MM:     \
+        return launch_runs_m##MM(a);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap)
+{
+    const size_t nb = (n + TPB - 1) / TPB, nbr = (err_cap + TPB - 1) / TPB;
+    return (nb + nbr) * 6 * (size_t)m;
+}
+
+}  // namespace msim

@@ -1,0 +1,40 @@
+// msim_kernels.h — host-side interface between the C ABI (msim_api.hip) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "msim_dispatch.h"
+
+namespace msim {
+
+struct LaunchArgs {
+    SimParams p;
+    uint64_t run_begin;
+    uint32_t n;
+    uint32_t seed_base;
+    uint64_t *partials;   // partials_words() u64
+    uint64_t *sums;       // 6*M u64 (msim_sums layout)
+    uint32_t *records;    // n*M*2 u32 or null
+    uint32_t *best_h;     // n u32 or null
+    uint32_t *err_count;  // 1 u32, zeroed before the launch
+    uint32_t *fail_count; // 1 u32, zeroed before the launch
+    uint32_t *err_list;   // err_cap u32
+    uint32_t err_cap;
+    uint32_t *status;     // 2 u32 or null
+    hipStream_t stream;
+};
+
+hipError_t launch_runs(const LaunchArgs &a);
+#define MSIM_DECL_LAUNCH(MM) hipError_t launch_runs_m##MM(const LaunchArgs &a);
+MSIM_FOR_EACH_M(MSIM_DECL_LAUNCH)
+#undef MSIM_DECL_LAUNCH
+// Launches msim_finalize (msim_common.hip): partial sums -> msim_sums, and the retry status words.
+hipError_t launch_finalize(const uint64_t *partials, uint32_t nparts, uint32_t nvals, uint64_t *out,
+                           const uint32_t *retry_count, const uint32_t *fail_count, uint32_t retry_cap,
+                           uint32_t *status, hipStream_t stream);
+hipError_t launch_log1p(const double *x, double *out, uint64_t n, hipStream_t s);
+hipError_t launch_intervals(const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s);
+hipError_t launch_picks(const SimParams &p, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
+constexpr int TPB = 256;  // 4 waves of 64 lanes per workgroup
+size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap);
+
+}  // namespace msim

@@ -30,8 +30,10 @@ namespace msim {
 
 constexpr int MAXM = 15;       // nibble 0xF is reserved for "no block"
 constexpr int WIN = 16;        // window heights (nibbles per u64)
-constexpr int NX = 4;          // extra in-flight honest blocks (beyond one per miner)
-constexpr int NG = 4;          // in-flight reveal groups of the selfish miner
+constexpr int NX_FAST = 4;     // extra in-flight honest blocks (beyond one per miner), fast kernel
+constexpr int NG_FAST = 4;     // in-flight reveal groups of the selfish miner, fast kernel
+constexpr int NX_WIDE = 12;    // ... retry kernel
+constexpr int NG_WIDE = 12;
 constexpr int FOLD_AT = WIN - 4;
 constexpr int64_t T_INF = 0x7FFFFFFFFFFFFFFFll;
 
@@ -89,7 +91,7 @@ MSIM_HD int pick_finder(const SimParams &p, uint64_t u)
     return k;
 }
 
-template <int M, bool SELF, bool DEEP>
+template <int M, bool SELF, bool DEEP, int NX = NX_FAST, int NG = NG_FAST>
 struct Sim {
     static_assert(M >= 1 && M <= MAXM, "miner count");
     uint64_t str[M];   // owners at window heights wb..wb+15 (0xF = none)

@@ -1,0 +1,194 @@
+"""Host-side mirror of the reference's configuration and driver surface, over libmsim's C ABI.
+
+Reference surface (/root/reference/main.cpp):
+  SIM_DURATION  main.cpp:7    months{12} = 31 556 952 000 ms
+  SIM_RUNS      main.cpp:10   16 * 2048
+  SetupMiners   main.cpp:44-65
+  MinerStats    main.cpp:13-41 (blocks_found, blocks_share, stale_rate; operator+=)
+  main          main.cpp:195-235 (batch driver + report)
+and Miner(id, perc, propagation, selfish=false) from simulation.h:57-59.
+
+Simulation.run() is the GPU replacement for main()'s std::async loop; report() prints main.cpp:224-234's
+lines so outputs can be diffed against the reference's stdout.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import MsimMiner, MsimRunRecord, MsimStats, MsimSums, check, lib
+
+SIM_DURATION_MS = 31_556_952_000  # main.cpp:7 std::chrono::months{12}
+SIM_RUNS = 16 * 2048              # main.cpp:10
+BLOCK_INTERVAL_MS = 600_000       # simulation.h:16
+DEFAULT_SEED_BASE = 1000          # SURVEY §8d seed convention
+
+
+@dataclass(frozen=True)
+class Miner:
+    """Miner(unsigned id, uint64_t perc, milliseconds prop, bool selfish) — simulation.h:57-59."""
+
+    id: int
+    perc: int
+    propagation_ms: int
+    is_selfish: bool = False
+
+
+def setup_miners(propagation_ms: int = 1000, selfish_perc: Optional[int] = None) -> List[Miner]:
+    """SetupMiners() (main.cpp:44-65): the 2025 hashrate approximation, homogeneous propagation.
+
+    With ``selfish_perc`` = h, miner 0 is selfish with h% and miner 1 gets 59-h% (README.md:85-107 uses
+    h = 40; SURVEY §8d C4 sweeps h over 10..49)."""
+    percs = [30, 29, 12, 11, 8, 5, 3, 1, 1]
+    selfish = False
+    if selfish_perc is not None:
+        percs[0], percs[1] = selfish_perc, 59 - selfish_perc
+        selfish = True
+    return [Miner(k, p, propagation_ms, selfish and k == 0) for k, p in enumerate(percs)]
+
+
+# BASELINE.json configs: C1 plumbing, C2 single-GPU bench, C3 selfish 40%.
+PRESETS = {
+    "c1": lambda: setup_miners(10_000),
+    "c2": lambda: setup_miners(100),
+    "c3": lambda: setup_miners(1_000, selfish_perc=40),
+    "default": lambda: setup_miners(1_000),
+}
+C4_SELFISH_PERCS = list(range(10, 50))
+C4_PROPAGATIONS_MS = [100, 250, 500, 1000, 2000, 5000, 10000, 20000, 30000]
+
+
+def c4_grid() -> List[List[Miner]]:
+    """The 360-point sweep of BASELINE.json configs[3]: h in 10..49 x propagation 0.1..30 s."""
+    return [setup_miners(p, selfish_perc=h) for h in C4_SELFISH_PERCS for p in C4_PROPAGATIONS_MS]
+
+
+@dataclass
+class MinerStats:
+    """MinerStats (main.cpp:13-41)."""
+
+    blocks_found: int = 0
+    blocks_share: float = 0.0
+    stale_rate: float = 0.0
+
+    def __iadd__(self, other: "MinerStats") -> "MinerStats":  # main.cpp:34-40
+        self.blocks_found += other.blocks_found
+        self.blocks_share += other.blocks_share
+        self.stale_rate += other.stale_rate
+        return self
+
+
+@dataclass
+class SimulationResult:
+    stats_total: List[MinerStats]              # like main.cpp:199 stats_total (sums over runs)
+    sums: List[MsimSums]                        # fixed-point device sums
+    found: Optional[np.ndarray] = None          # [n_runs, M] uint32, per-run blocks_found
+    stale: Optional[np.ndarray] = None          # [n_runs, M] uint32, per-run stale_blocks
+    best_height: Optional[np.ndarray] = None    # [n_runs] uint32, |best chain| - 1
+    n_runs: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+def _miners_struct(miners: Sequence[Miner]):
+    arr = (MsimMiner * len(miners))()
+    for i, m in enumerate(miners):
+        arr[i] = MsimMiner(m.id, m.perc, m.propagation_ms, 1 if m.is_selfish else 0)
+    return arr
+
+
+class Simulation:
+    """A network description bound to the device library (msim_config)."""
+
+    def __init__(self, miners: Sequence[Miner], duration_ms: int = SIM_DURATION_MS):
+        self.miners = list(miners)
+        self.duration_ms = int(duration_ms)
+        handle = ctypes.c_void_p()
+        check(lib.msim_config_create(_miners_struct(self.miners), len(self.miners), self.duration_ms,
+                                     ctypes.byref(handle)), "msim_config_create")
+        self._h = handle
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.msim_config_destroy(h)
+            self._h = None
+
+    def run(self, n_runs: int, run_begin: int = 0, seed_base: int = DEFAULT_SEED_BASE, device: int = 0,
+            per_run: bool = False) -> SimulationResult:
+        m = len(self.miners)
+        stats = (MsimStats * m)()
+        sums = (MsimSums * m)()
+        rec = (MsimRunRecord * (n_runs * m))() if per_run else None
+        bh = (ctypes.c_uint32 * n_runs)() if per_run else None
+        check(lib.msim_run(self._h, run_begin, n_runs, seed_base & 0xFFFFFFFF, device, stats, sums, rec, bh), "msim_run")
+        res = SimulationResult(
+            stats_total=[MinerStats(s.blocks_found, s.blocks_share, s.stale_rate) for s in stats],
+            sums=list(sums),
+            n_runs=n_runs,
+        )
+        if per_run:
+            a = np.ctypeslib.as_array(ctypes.cast(rec, ctypes.POINTER(ctypes.c_uint32)), shape=(n_runs, m, 2)).copy()
+            res.found = a[:, :, 0]
+            res.stale = a[:, :, 1]
+            res.best_height = np.ctypeslib.as_array(bh).copy()
+        return res
+
+    # ---- device-resident form (torch tensors as HBM buffers; used by bench.py and the RCCL path)
+    def workspace_bytes(self, n_runs: int) -> int:
+        return int(lib.msim_workspace_bytes(self._h, n_runs))
+
+    def launch(self, n_runs: int, run_begin: int, seed_base: int, d_sums, d_workspace, d_status,
+               d_per_run=None, d_best_height=None, stream=None) -> None:
+        """Asynchronous launch on the current device: all buffers are torch CUDA (HIP) tensors.
+
+        d_sums: int64 [M, 6] (msim_sums); d_status: int32 [2]; d_workspace: uint8 [workspace_bytes]."""
+        ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+        sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        check(lib.msim_launch(self._h, run_begin, n_runs, seed_base & 0xFFFFFFFF, ptr(d_sums), ptr(d_per_run),
+                              ptr(d_best_height), ptr(d_status), ptr(d_workspace), d_workspace.numel(), sh),
+              "msim_launch")
+
+
+def sums_to_stats(sums_rows: Iterable[Sequence[int]]) -> List[MinerStats]:
+    """Fixed-point msim_sums rows ([found, stale, share_hi, share_lo, rate_hi, rate_lo]) -> MinerStats."""
+    out = []
+    for r in sums_rows:
+        found, _stale, sh, sl, rh, rl = (int(x) for x in r)
+        out.append(MinerStats(found, float(sh) + float(sl) * 2.0 ** -32, float(rh) + float(rl) * 2.0 ** -32))
+    return out
+
+
+def exact_stats_total(found: np.ndarray, stale: np.ndarray, best_height: np.ndarray) -> List[MinerStats]:
+    """MinerStats per run (main.cpp:22-30) summed in run order (main.cpp:211-217), bit-exact."""
+    n, m = found.shape
+    tot = [MinerStats() for _ in range(m)]
+    for r in range(n):
+        L = float(best_height[r])
+        for k in range(m):
+            f = int(found[r, k])
+            share = 0.0 if f == 0 else f / L
+            rate = 0.0 if f == 0 else int(stale[r, k]) / f
+            tot[k] += MinerStats(f, share, rate)
+    return tot
+
+
+def report(miners: Sequence[Miner], stats_total: Sequence[MinerStats], sim_runs: int,
+           duration_ms: int = SIM_DURATION_MS) -> str:
+    """The report lines of main.cpp:224-234 (iostream default float format = %g, 6 digits)."""
+    days = duration_ms // 86_400_000
+    lines = [f"After running {sim_runs} simulations for {days}d each, on average:"]
+    for m, s in zip(miners, stats_total):
+        line = (f"  - Miner {m.id} ({m.perc}% of network hashrate) found {int(s.blocks_found) // sim_runs} blocks i.e. "
+                f"{s.blocks_share * 100 / sim_runs:.6g}% of blocks. Stale rate: {s.stale_rate * 100 / sim_runs:.6g}%.")
+        if m.is_selfish:
+            line += " ('selfish mining' strategy)"
+        lines.append(line)
+    return "\n".join(lines)

@@ -476,3 +476,18 @@ void oracle_state_notify(oracle_miner_state *s, const uint32_t *ids, const int64
 
 int64_t oracle_selfish_arrival(void) { return OR_SELFISH_ARRIVAL; }
 uint32_t oracle_genesis_id(void) { return OR_GENESIS_ID; }
+
+/* Array helpers for tests: glibc log1p and NextBlockInterval of given uniforms (simulation.h:205-210). */
+void oracle_log1p_array(const double *x, double *out, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) out[i] = log1p(x[i]);
+}
+
+void oracle_interval_of_array(const uint64_t *u, int64_t *out, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) {
+        const double e = -log1p((double)(u[i] >> 11) * -0x1.0p-53);
+        const long long ns = llround((double)OR_BLOCK_INTERVAL_NS * e);
+        out[i] = (int64_t)(ns / 1000000LL);
+    }
+}

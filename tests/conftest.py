@@ -1,0 +1,47 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+def _ensure(path: str, builder) -> None:
+    if not os.path.exists(path):
+        builder()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import pyoracle
+
+    _ensure(pyoracle.LIB, pyoracle.build)
+    return pyoracle
+
+
+@pytest.fixture(scope="session")
+def native_tests():
+    """Test-only host builds: build/libmodel_host.so and build/draws_check."""
+    import __graft_entry__ as ge
+
+    lib = os.path.join(ROOT, "build", "libmodel_host.so")
+    chk = os.path.join(ROOT, "build", "draws_check")
+    if not (os.path.exists(lib) and os.path.exists(chk)):
+        ge.build_native_tests()
+    return {"model_host": lib, "draws_check": chk}
+
+
+@pytest.fixture(scope="session")
+def msim_lib_path():
+    path = os.path.join(ROOT, "miningsimulation_amd", "libmsim.so")
+    if not os.path.exists(path):
+        jobs = str(max(1, min(16, os.cpu_count() or 8)))
+        subprocess.run(["make", "-s", f"-j{jobs}", "-C", os.path.join(ROOT, "miningsimulation_amd", "csrc")], check=True)
+    return path

@@ -1,0 +1,70 @@
+"""The C-ABI library loads and exports every symbol include/msim.h declares (no GPU calls), and the
+ctypes structs match the header's layouts."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    with open(os.path.join(ROOT, "include", "msim.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(msim_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol(msim_lib_path):
+    lib = ctypes.CDLL(msim_lib_path)
+    declared = _declared()
+    assert len(declared) >= 12
+    for name in declared:
+        assert hasattr(lib, name), name
+
+
+def test_python_binding_covers_header(msim_lib_path):
+    from miningsimulation_amd import _lib
+
+    assert sorted(_lib.EXPORTED) == _declared()
+
+
+def test_struct_layouts(msim_lib_path):
+    from miningsimulation_amd import _lib
+
+    assert ctypes.sizeof(_lib.MsimStats) == 24  # MinerStats: long, double, double (main.cpp:13-20)
+    assert ctypes.sizeof(_lib.MsimSums) == 48
+    assert ctypes.sizeof(_lib.MsimRunRecord) == 8
+    assert ctypes.sizeof(_lib.MsimMiner) == 32
+
+
+def test_config_validation_without_gpu(msim_lib_path):
+    """Config creation is host-only: the reference's asserted preconditions become error codes."""
+    from miningsimulation_amd import Miner, MsimError, Simulation, setup_miners
+    from miningsimulation_amd import _lib
+
+    Simulation(setup_miners())  # valid
+    bad = [
+        ([Miner(0, 60, 1000), Miner(1, 30, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 90
+        ([Miner(0, 60, 1000), Miner(1, 50, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 110
+        ([Miner(0, 50, 1000, True), Miner(1, 50, 1000, True)], _lib.MSIM_E_SELFISH),
+        ([Miner(0, 50, 1000), Miner(0, 50, 1000)], _lib.MSIM_E_MINERS),             # duplicate id
+        ([Miner(k, 6 if k < 10 else 5, 1000) for k in range(16)], _lib.MSIM_E_MINERS),
+        ([Miner(0, 50, -1), Miner(1, 50, 1000)], _lib.MSIM_E_INVALID),
+    ]
+    for miners, code in bad:
+        try:
+            Simulation(miners)
+        except MsimError as e:
+            assert e.code == code, (miners, e)
+        else:
+            raise AssertionError(f"accepted invalid network {miners}")
+
+
+def test_report_format():
+    from miningsimulation_amd import MinerStats, report, setup_miners
+
+    miners = setup_miners(10_000)
+    # README.md:55-56 first line, from its printed averages
+    st = [MinerStats(15621 * 32768, 0.300901 * 32768, 0.010092 * 32768)] + [MinerStats()] * 8
+    out = report(miners, st, 32768).splitlines()
+    assert out[0] == "After running 32768 simulations for 365d each, on average:"
+    assert out[1] == "  - Miner 0 (30% of network hashrate) found 15621 blocks i.e. 30.0901% of blocks. Stale rate: 1.0092%."

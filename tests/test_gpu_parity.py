@@ -1,0 +1,191 @@
+"""Parity of the gfx950 path (libmsim.so through its C ABI) against the CPU oracle and golden vectors.
+
+Bar: bit-exact per-run integer counters (found, stale, best-chain height) for identical seeds; f64
+aggregates from per-run records bit-exact against the oracle's run-order sums (main.cpp:211-217);
+fixed-point device sums within 1e-9 relative of those; sizes where the oracle cannot follow are checked
+through size-independent invariants."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+D = 31_556_952_000
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def msim(msim_lib_path):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.cuda.set_device(0)
+    import miningsimulation_amd as m
+
+    return m
+
+
+def _sim(msim, percs, props, selfish, duration=D):
+    miners = [msim.Miner(k, percs[k], props[k], bool(selfish[k])) for k in range(len(percs))]
+    return msim.Simulation(miners, duration)
+
+
+def test_gpu_log1p_and_intervals(msim, oracle):
+    """glibc log1p and NextBlockInterval on the device, bit for bit (xoroshiro128++.h:19, simulation.h:205-210)."""
+    import ctypes
+
+    import torch
+    from miningsimulation_amd import _lib
+
+    rng = np.random.default_rng(5)
+    n = 1 << 22
+    u = rng.integers(0, 2**64 - 1, size=n, dtype=np.uint64, endpoint=True)
+    # plus both ends of the domain and the branch thresholds of the fdlibm algorithm
+    edge = np.concatenate([np.arange(4096, dtype=np.uint64) << np.uint64(11),
+                           ((np.uint64(2**53 - 1) - np.arange(4096, dtype=np.uint64)) << np.uint64(11))])
+    u = np.concatenate([u, edge])
+    x = (u >> np.uint64(11)).astype(np.float64) * -(2.0**-53)
+    du = torch.from_numpy(u.view(np.int64)).cuda()
+    dx = torch.from_numpy(x).cuda()
+    dl = torch.empty_like(dx)
+    di = torch.empty(u.size, dtype=torch.int64, device="cuda")
+    _lib.check(_lib.lib.msim_device_log1p(ctypes.c_void_p(dx.data_ptr()), ctypes.c_void_p(dl.data_ptr()), u.size, None))
+    _lib.check(_lib.lib.msim_device_intervals(ctypes.c_void_p(du.data_ptr()), ctypes.c_void_p(di.data_ptr()), u.size, None))
+    torch.cuda.synchronize()
+    ref_l = oracle.log1p_array(x)
+    ref_i = oracle.interval_of_array(u)
+    assert np.array_equal(dl.cpu().numpy().view(np.uint64), ref_l.view(np.uint64))
+    assert np.array_equal(di.cpu().numpy(), ref_i)
+
+
+def test_gpu_picks(msim, oracle):
+    import ctypes
+
+    import torch
+    from miningsimulation_amd import _lib
+
+    percs = [30, 29, 12, 11, 8, 5, 3, 1, 1]
+    sim = _sim(msim, percs, [1000] * 9, [0] * 9)
+    words = np.array(oracle.rng_stream(7, 4096), dtype=np.uint64)
+    du = torch.from_numpy(words.view(np.int64)).cuda()
+    dk = torch.empty(words.size, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.msim_device_picks(sim.handle, ctypes.c_void_p(du.data_ptr()), ctypes.c_void_p(dk.data_ptr()),
+                                          words.size, None))
+    torch.cuda.synchronize()
+    assert dk.cpu().tolist() == oracle.picks(percs, 7, 4096)
+
+
+@pytest.mark.parametrize("name", ["c1_prop10s", "c2_prop100ms", "default_prop1s", "c3_selfish40_prop1s",
+                                  "c4_selfish49_prop30s", "c4_selfish10_prop100ms"])
+def test_gpu_golden_vectors(msim, name):
+    """64 full-year runs per configuration, per-run counters identical to tests/golden/oracle_vectors.npz."""
+    z = np.load(os.path.join(GOLD, "oracle_vectors.npz"))
+    p, q, s = z[name + "_config"].tolist()
+    res = _sim(msim, p, q, s).run(64, 0, 1000, 0, per_run=True)
+    assert np.array_equal(res.found.astype(np.int64), z[name + "_found"])
+    assert np.array_equal(res.stale.astype(np.int64), z[name + "_stale"])
+    assert np.array_equal(res.best_height.astype(np.int64), z[name + "_best_height"])
+
+
+@pytest.mark.parametrize("preset", ["c1", "c2", "c3", "default"])
+def test_gpu_presets_vs_oracle(msim, oracle, preset):
+    """512 runs of each BASELINE configuration vs the oracle, run by run, plus the f64 aggregate."""
+    miners = msim.PRESETS[preset]()
+    p = [m.perc for m in miners]
+    q = [m.propagation_ms for m in miners]
+    s = [m.is_selfish for m in miners]
+    n, begin = 512, 4096
+    res = _sim(msim, p, q, s).run(n, begin, 1000, 0, per_run=True)
+    f, st, sh, r = oracle.run_batch(p, q, s, D, n, begin, 1000, threads=16)
+    assert np.array_equal(res.found.astype(np.int64), f)
+    assert np.array_equal(res.stale.astype(np.int64), st)
+    for k in range(len(p)):
+        # exact run-order sums (main.cpp:211-217)
+        ref_share = 0.0
+        ref_rate = 0.0
+        for i in range(n):
+            ref_share += sh[i, k]
+            ref_rate += r[i, k]
+        assert res.stats_total[k].blocks_found == int(f[:, k].sum())
+        assert res.stats_total[k].blocks_share == ref_share
+        assert res.stats_total[k].stale_rate == ref_rate
+        # fixed-point device sums
+        fx = msim.sums_to_stats([[res.sums[k].blocks_found, res.sums[k].stale_blocks, res.sums[k].share_hi,
+                                  res.sums[k].share_lo, res.sums[k].rate_hi, res.sums[k].rate_lo]])[0]
+        assert abs(fx.blocks_share - ref_share) <= 1e-9 * max(1.0, ref_share)
+        assert abs(fx.stale_rate - ref_rate) <= 1e-9 * max(1.0, ref_rate) + n * 2.0**-32
+
+
+def test_gpu_random_networks(msim, oracle):
+    """Random networks (1-15 miners, mixed delays incl. 0 ms, honest or one selfish), 64 runs each."""
+    rng = random.Random(2024)
+    for _ in range(24):
+        m = rng.randint(1, 15)
+        cuts = sorted(rng.sample(range(1, 100), m - 1)) if m > 1 else []
+        b = [0] + cuts + [100]
+        p = [b[i + 1] - b[i] for i in range(m)]
+        q = [rng.choice([0, 1, 100, 1000, 10_000, 30_000]) for _ in range(m)]
+        sidx = rng.randrange(m) if (m > 1 and rng.random() < 0.5) else -1
+        s = [k == sidx for k in range(m)]
+        dur = rng.choice([10**8, 10**9, 10**10])
+        seed = rng.randrange(2**32)
+        res = _sim(msim, p, q, s, dur).run(64, 0, seed, 0, per_run=True)
+        f, st, _, _ = oracle.run_batch(p, q, s, dur, 64, 0, seed, threads=16)
+        assert np.array_equal(res.found.astype(np.int64), f), (p, q, s, dur, seed)
+        assert np.array_equal(res.stale.astype(np.int64), st), (p, q, s, dur, seed)
+
+
+def test_gpu_c4_grid_sample(msim, oracle):
+    """A sample of the 360-point sweep (BASELINE configs[3]) at full length, 32 runs per point."""
+    rng = random.Random(7)
+    grid = msim.c4_grid()
+    for miners in rng.sample(grid, 10):
+        p = [m.perc for m in miners]
+        q = [m.propagation_ms for m in miners]
+        s = [m.is_selfish for m in miners]
+        res = _sim(msim, p, q, s).run(32, 0, 1000, 0, per_run=True)
+        f, st, _, _ = oracle.run_batch(p, q, s, D, 32, 0, 1000, threads=16)
+        assert np.array_equal(res.found.astype(np.int64), f), (p, q)
+        assert np.array_equal(res.stale.astype(np.int64), st), (p, q)
+
+
+def test_gpu_retry_path_huge_delays(msim, oracle):
+    """Delays of minutes overflow the fast kernel's in-flight capacity; the retry kernel must take those
+    runs and still match the oracle."""
+    p = [30, 29, 12, 11, 8, 5, 3, 1, 1]
+    q = [300_000] * 9
+    s = [False] * 9
+    res = _sim(msim, p, q, s, 10**10).run(128, 0, 1000, 0, per_run=True)
+    f, st, _, _ = oracle.run_batch(p, q, s, 10**10, 128, 0, 1000, threads=16)
+    assert np.array_equal(res.found.astype(np.int64), f)
+    assert np.array_equal(res.stale.astype(np.int64), st)
+
+
+def test_gpu_sharding_is_exact(msim):
+    """Integer sums are partition-independent: [0,N) == [0,N/2) + [N/2,N), bit for bit (what makes the
+    1/2/4/8-GPU all-reduce results identical)."""
+    sim = _sim(msim, [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [1] + [0] * 8)
+    n = 8192
+    whole = sim.run(n, 0, 1000, 0)
+    a = sim.run(n // 2, 0, 1000, 0)
+    b = sim.run(n // 2, n // 2, 1000, 0)
+    for k in range(9):
+        for fld in ("blocks_found", "stale_blocks", "share_hi", "share_lo", "rate_hi", "rate_lo"):
+            assert getattr(whole.sums[k], fld) == getattr(a.sums[k], fld) + getattr(b.sums[k], fld)
+
+
+def test_gpu_invariants_full_scale(msim):
+    """BASELINE configs[1] at full size (32768 runs x 365 d, one launch): no failed run; per-run
+    sum of found = best height (the genesis block has no owner, main.cpp:27-28); the aggregate matches
+    README.md:72,80 within Monte-Carlo error."""
+    miners = msim.PRESETS["c2"]()
+    res = msim.Simulation(miners).run(32768, 0, 1000, 0, per_run=True)
+    assert np.array_equal(res.found.sum(axis=1).astype(np.int64), res.best_height.astype(np.int64))
+    n = 32768
+    share0 = res.stats_total[0].blocks_share * 100 / n
+    rate0 = res.stats_total[0].stale_rate * 100 / n
+    assert abs(share0 - 30.0008) < 0.02
+    assert abs(rate0 - 0.0101929) < 0.0015
