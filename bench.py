@@ -36,13 +36,20 @@ def w_blk(m: int) -> int:
     return 140 + 4 * math.ceil(math.log2(max(m, 2)))
 
 
-def cpu_baseline(preset: str, sample_runs: int, threads: int) -> dict:
+def cpu_baseline(preset: str, sample_runs: int, threads: int, target_s: float = 15.0) -> dict:
     from oracle import pyoracle
 
     pyoracle.build()
-    out = subprocess.run([pyoracle.CLI, "time", preset, str(sample_runs), str(threads)], capture_output=True,
-                         text=True, check=True)
-    rec = json.loads(out.stdout.splitlines()[0])
+
+    def timed(runs: int) -> dict:
+        out = subprocess.run([pyoracle.CLI, "time", preset, str(runs), str(threads)], capture_output=True,
+                             text=True, check=True)
+        return json.loads(out.stdout.splitlines()[0])
+
+    if not sample_runs:  # calibrate on a small sample, then size the real sample to ~target_s seconds
+        probe = timed(threads * 16)
+        sample_runs = max(threads * 16, int(probe["run_years_per_s"] * target_s) // threads * threads)
+    rec = timed(sample_runs)
     return {
         "value": round(rec["run_years_per_s"], 2),
         "unit": "run-years/s",
@@ -170,8 +177,7 @@ def main() -> None:
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(16, os.cpu_count() or 1))
-            sample = args.cpu_sample_runs or threads * 96
-            line["cpu_baseline"] = cpu_baseline(args.config, sample, threads)
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_runs, threads)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
