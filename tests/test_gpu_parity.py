@@ -189,3 +189,21 @@ def test_gpu_invariants_full_scale(msim):
     rate0 = res.stats_total[0].stale_rate * 100 / n
     assert abs(share0 - 30.0008) < 0.02
     assert abs(rate0 - 0.0101929) < 0.0015
+
+
+def test_host_dropin_driver(msim):
+    """host/msim_main (the C++ drop-in for main.cpp) prints main.cpp:224-234's report; its numbers equal
+    the Python host path's fixed-point sums for the same runs."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(GOLD), "..", "host", "msim_main")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(GOLD), "..", "host")], check=True)
+    out = subprocess.run([exe, "1", "1000"], capture_output=True, text=True, check=True).stdout.splitlines()
+    assert out[0] == "Running 32768 simulations in parallel using 1 GPU(s)."
+    assert out[2] == "After running 32768 simulations for 365d each, on average:"
+    miners = msim.setup_miners(1000)
+    res = msim.Simulation(miners).run(32768, 0, 1000, 0)
+    rows = [[s.blocks_found, s.stale_blocks, s.share_hi, s.share_lo, s.rate_hi, s.rate_lo] for s in res.sums]
+    want = msim.report(miners, msim.sums_to_stats(rows), 32768).splitlines()
+    assert out[2:] == want
