@@ -96,8 +96,10 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
 
 /* Device draw primitives (bit-exact with the reference's host libm; test and sampler surface):
  *   msim_device_log1p     glibc log1p on the reference's domain (xoroshiro128++.h:19)
- *   msim_device_intervals NextBlockInterval of given uniform u64 draws, in ms (simulation.h:205-210)
- *   msim_device_picks     PickFinder index of given uniform u64 draws (simulation.h:213-221)
+ *   msim_device_intervals NextBlockInterval of given uniform u64 draws, in ms (simulation.h:205-210),
+ *                         through the draw kernel's production path (msim_fastdraw.h + exact fallback)
+ *   msim_device_picks     PickFinder index of given uniform u64 draws (simulation.h:213-221), through
+ *                         the draw kernel's table lookup; -1 where the reference would assert
  * All pointers are device memory; launches go to `stream` (hipStream_t, NULL = default). */
 int msim_device_log1p(const double *d_x, double *d_out, uint64_t n, void *stream);
 int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t n, void *stream);

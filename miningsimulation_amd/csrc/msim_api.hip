@@ -5,18 +5,32 @@
 // and sums MinerStats in run order on the main thread. Here one launch runs a whole shard of runs,
 // one run per lane, and the per-miner sums are reduced on the device in integers.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "../../include/msim.h"
+#include "msim_jump.h"
 #include "msim_kernels.h"
+
+namespace {
+constexpr int MAX_DEVICES = 64;
+}
 
 struct msim_config {
     msim::SimParams p;
     uint32_t n;
     uint32_t ids[MSIM_MAX_MINERS];
+    uint64_t perc[MSIM_MAX_MINERS];
+    int64_t prop[MSIM_MAX_MINERS];
+    uint8_t self[MSIM_MAX_MINERS];
+    double rho;      // probability that a block is not "fast" (msim_pipeline.h)
+    bool pipe_ok;    // event-skipping pipeline eligible (honest network, rare forks)
+    std::mutex mu;
+    void *tables[MAX_DEVICES];  // per-device pipeline tables (lazily uploaded)
 };
 
 namespace {
@@ -46,6 +60,65 @@ WsLayout ws_layout(uint32_t m, uint64_t n)
 }
 
 constexpr uint64_t MAX_LAUNCH_RUNS = 1ull << 26;
+constexpr double PIPE_MAX_RHO = 0.08;           // above this the per-lane kernel is cheaper
+constexpr double PIPE_SLICE_BUDGET = 16.0 * (1ull << 30);  // pipeline workspace per slice (bytes)
+
+msim::PipeLayout pipe_layout(const msim_config *c, uint64_t n_runs)
+{
+    return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET);
+}
+
+// Pipeline tables for this config on the current device: pick table, log table, jump matrices.
+int device_tables(msim_config *c, uint32_t nseg, msim::PipeTables *out)
+{
+    using namespace msim;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) return MSIM_E_HIP;
+    std::lock_guard<std::mutex> g(c->mu);
+    const size_t pick_b = PICK_TAB * sizeof(PickEntry), log_b = LOG_TAB * sizeof(LogEntry);
+    if (!c->tables[dev]) {
+        const size_t jump_b = (size_t)nseg * 128 * 16;
+        std::vector<char> h(pick_b + log_b + jump_b);
+        build_pick_table(c->perc, c->prop, c->self, (int)c->n, (PickEntry *)h.data());
+        build_log_table((LogEntry *)(h.data() + pick_b));
+        build_jump_table(nseg, SEG, (uint32_t *)(h.data() + pick_b + log_b));
+        void *d = nullptr;
+        if (hipMalloc(&d, h.size()) != hipSuccess) return MSIM_E_HIP;
+        if (hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return MSIM_E_HIP;
+        }
+        c->tables[dev] = d;
+    }
+    const char *d = (const char *)c->tables[dev];
+    out->pick = (const PickEntry *)d;
+    out->logt = (const LogEntry *)(d + pick_b);
+    out->jump = (const uint32_t *)(d + pick_b + log_b);
+    return MSIM_OK;
+}
+
+// Process-wide log table (msim_fastdraw.h) per device, for msim_device_intervals.
+int global_log_table(const msim::LogEntry **out)
+{
+    static std::mutex mu;
+    static void *tab[MAX_DEVICES] = {nullptr};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) return MSIM_E_HIP;
+    std::lock_guard<std::mutex> g(mu);
+    if (!tab[dev]) {
+        msim::LogEntry h[msim::LOG_TAB];
+        msim::build_log_table(h);
+        void *d = nullptr;
+        if (hipMalloc(&d, sizeof(h)) != hipSuccess) return MSIM_E_HIP;
+        if (hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return MSIM_E_HIP;
+        }
+        tab[dev] = d;
+    }
+    *out = (const msim::LogEntry *)tab[dev];
+    return MSIM_OK;
+}
 
 }  // namespace
 
@@ -71,27 +144,46 @@ int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms
     }
     // "Must add up to 1" (main.cpp:43); anything else makes PickFinder assert (simulation.h:220).
     if (total != 100) return MSIM_E_WEIGHTS;
-    msim_config *c = (msim_config *)calloc(1, sizeof(msim_config));
+    msim_config *c = new (std::nothrow) msim_config();
     if (!c) return MSIM_E_INVALID;
     const int rc = msim::make_params(perc, prop, self, (int)n, duration_ms, &c->p);
     if (rc) {
-        free(c);
+        delete c;
         return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
     }
     c->n = n;
-    for (uint32_t k = 0; k < n; ++k) c->ids[k] = miners[k].id;
+    double rho = 0.0;
+    for (uint32_t k = 0; k < n; ++k) {
+        c->ids[k] = miners[k].id;
+        c->perc[k] = perc[k];
+        c->prop[k] = prop[k];
+        c->self[k] = self[k];
+        // P(next interval <= prop): the block is not fast (msim_pipeline.h)
+        rho += (double)perc[k] / 100.0 * (self[k] ? 1.0 : 1.0 - exp(-((double)prop[k] + 1.0) / 599999.5));
+    }
+    c->rho = rho;
+    c->pipe_ok = c->p.selfish < 0 && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
+    for (int d = 0; d < MAX_DEVICES; ++d) c->tables[d] = nullptr;
     *out = c;
     return MSIM_OK;
 }
 
-void msim_config_destroy(msim_config *cfg) { free(cfg); }
+void msim_config_destroy(msim_config *cfg)
+{
+    if (!cfg) return;
+    for (int d = 0; d < MAX_DEVICES; ++d)
+        if (cfg->tables[d]) (void)hipFree(cfg->tables[d]);
+    delete cfg;
+}
 
 uint32_t msim_config_miner_count(const msim_config *cfg) { return cfg ? cfg->n : 0; }
 
 size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
 {
     if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
-    return ws_layout(cfg->n, n_runs).total;
+    size_t t = ws_layout(cfg->n, n_runs).total;
+    if (cfg->pipe_ok) t += pipe_layout(cfg, n_runs).total;
+    return t;
 }
 
 int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, void *d_sums,
@@ -100,7 +192,9 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
 {
     if (!cfg || !d_sums || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
     const WsLayout l = ws_layout(cfg->n, n_runs);
-    if (workspace_bytes < l.total) return MSIM_E_INVALID;
+    msim::PipeLayout pl;
+    if (cfg->pipe_ok) pl = pipe_layout(cfg, n_runs);
+    if (workspace_bytes < l.total + (cfg->pipe_ok ? pl.total : 0)) return MSIM_E_INVALID;
     char *ws = (char *)d_workspace;
     hipStream_t s = (hipStream_t)stream;
     uint32_t *counts = (uint32_t *)(ws + l.counts_off);
@@ -120,6 +214,14 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
     a.err_cap = l.err_cap;
     a.status = (uint32_t *)d_status;
     a.stream = s;
+    a.pl = nullptr;
+    a.pipe_ws = nullptr;
+    if (cfg->pipe_ok) {
+        const int rc = device_tables(const_cast<msim_config *>(cfg), pl.nseg, &a.tab);
+        if (rc) return rc;
+        a.pl = &pl;
+        a.pipe_ws = ws + l.total;
+    }
     return msim::launch_runs(a) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
 }
 
@@ -132,13 +234,19 @@ int msim_device_log1p(const double *d_x, double *d_out, uint64_t n, void *stream
 int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t n, void *stream)
 {
     if (!d_uniform || !d_out_ms) return MSIM_E_INVALID;
-    return msim::launch_intervals(d_uniform, d_out_ms, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+    const msim::LogEntry *lt = nullptr;
+    const int rc = global_log_table(&lt);
+    if (rc) return rc;
+    return msim::launch_intervals(lt, d_uniform, d_out_ms, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
 }
 
 int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t *d_out_index, uint64_t n, void *stream)
 {
     if (!cfg || !d_uniform || !d_out_index) return MSIM_E_INVALID;
-    return msim::launch_picks(cfg->p, d_uniform, d_out_index, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+    msim::PipeTables t;
+    const int rc = device_tables(const_cast<msim_config *>(cfg), pipe_layout(cfg, 1).nseg, &t);
+    if (rc) return rc;
+    return msim::launch_picks(t.pick, d_uniform, d_out_index, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
 }
 
 void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out)
@@ -157,7 +265,7 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
     if (hipSetDevice(device) != hipSuccess) return MSIM_E_HIP;
     const uint32_t m = cfg->n;
     const uint64_t chunk = n_runs < MAX_LAUNCH_RUNS ? n_runs : MAX_LAUNCH_RUNS;
-    const size_t wsb = ws_layout(m, chunk).total;
+    const size_t wsb = msim_workspace_bytes(cfg, chunk);
     void *ws = nullptr, *sums = nullptr, *status = nullptr, *rec = nullptr, *bh = nullptr;
     const bool want_rec = opt_per_run != nullptr;
     const bool want_bh = want_rec || opt_best_height != nullptr;

@@ -28,40 +28,10 @@ __global__ void msim_log1p_kernel(const double *__restrict__ x, double *__restri
     if (i < n) out[i] = glibc_log1p(x[i]);
 }
 
-__global__ void msim_interval_kernel(const uint64_t *__restrict__ u, int64_t *__restrict__ out, uint64_t n)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = interval_ms_of(u[i]);
-}
-
-__global__ void msim_pick_kernel(const SimParams p, const uint64_t *__restrict__ u, int32_t *__restrict__ out, uint64_t n)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    // PickFinder's running sum (simulation.h:216-218) over the runtime miner count.
-    int k = 0;
-    for (int j = 0; j < p.m; ++j) k += (p.thresh[j] <= u[i]) ? 1 : 0;
-    out[i] = k < p.m ? k : -1;
-}
-
 hipError_t launch_log1p(const double *x, double *out, uint64_t n, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(msim_log1p_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, out, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_intervals(const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s)
-{
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(msim_interval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, out, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_picks(const SimParams &p, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
-{
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(msim_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, u, out, n);
     return hipGetLastError();
 }
 

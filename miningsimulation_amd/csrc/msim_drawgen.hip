@@ -1,0 +1,159 @@
+// msim_drawgen.hip — K1 of the event-skipping pipeline (msim_pipeline.h): every block's draws.
+//
+// One lane = (run, segment): both of the run's xoroshiro128++ streams (main.cpp:134) are jumped to
+// draw j*SEG (msim_jump.h), then the lane produces SEG blocks exactly as the reference's sequential
+// loop would draw them (simulation.h:205-221): interval I_i (ms), finder k_i, and the "fast" bit
+// I_{i+1} > prop_{k_i} (honest finders only). A wave = 64 consecutive runs at one segment, so the
+// jump matrix columns are wave-uniform scalar loads and every 4-block store is one coalesced 1 KiB
+// wave store. Roofline: VALU issue (FP64 log + 64-bit integer RNG); the word stream is 4 B/block.
+#include <hip/hip_runtime.h>
+
+#include "msim_jump.h"
+#include "msim_kernels.h"
+#include "msim_pipeline.h"
+
+namespace msim {
+
+__device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
+
+// Both RNG states of the lane advanced by the same jump matrix (128 wave-uniform columns).
+__device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rng &b)
+{
+    const uint32_t sa[4] = {(uint32_t)a.s0, (uint32_t)(a.s0 >> 32), (uint32_t)a.s1, (uint32_t)(a.s1 >> 32)};
+    const uint32_t sb[4] = {(uint32_t)b.s0, (uint32_t)(b.s0 >> 32), (uint32_t)b.s1, (uint32_t)(b.s1 >> 32)};
+    uint32_t oa0 = 0, oa1 = 0, oa2 = 0, oa3 = 0, ob0 = 0, ob1 = 0, ob2 = 0, ob3 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) {
+            const uint4 c = cols[w * 32 + i];
+            const uint32_t ma = 0u - ((sa[w] >> i) & 1u), mb = 0u - ((sb[w] >> i) & 1u);
+            oa0 ^= c.x & ma;
+            oa1 ^= c.y & ma;
+            oa2 ^= c.z & ma;
+            oa3 ^= c.w & ma;
+            ob0 ^= c.x & mb;
+            ob1 ^= c.y & mb;
+            ob2 ^= c.z & mb;
+            ob3 ^= c.w & mb;
+        }
+    }
+    a.s0 = (uint64_t)oa0 | ((uint64_t)oa1 << 32);
+    a.s1 = (uint64_t)oa2 | ((uint64_t)oa3 << 32);
+    b.s0 = (uint64_t)ob0 | ((uint64_t)ob1 << 32);
+    b.s1 = (uint64_t)ob2 | ((uint64_t)ob3 << 32);
+}
+
+// Side effects of one K1 lane (msim_pipeline.h draw_segment): LDS per-owner counters, coalesced
+// word stores, wave-aggregated appends to the dense episode list.
+struct DevCtx {
+    const DrawArgs &a;
+    uint32_t (*cnt)[256];
+    uint32_t tid, lane, r, seg, jb, nsl;
+    bool active;
+    uint4 *wout;
+    __device__ void count(uint32_t k) { atomicAdd(&cnt[k >> 1][tid], 1u << (16u * (k & 1u))); }
+    __device__ void slow(bool is_slow, uint32_t block, uint64_t offset)
+    {
+        const bool want = is_slow && active;
+        const uint64_t mask = __ballot(want);
+        if (!mask) return;  // wave-uniform
+        const int leader = __ffsll((unsigned long long)mask) - 1;
+        uint32_t base = 0;
+        if ((int)lane == leader) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
+        base = __shfl(base, leader, 64);
+        if (!want) return;
+        const uint32_t idx =
+            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (idx < a.lcap) {
+            EpEntry e;
+            e.run = r;
+            e.block = block;
+            e.offset = offset;
+            a.list[idx] = e;
+        }
+        if (nsl < a.cap) a.slots[((size_t)seg * a.cap + nsl) * a.nr + r] = idx;
+        ++nsl;
+    }
+    __device__ void store4(uint32_t q4, uint32_t x, uint32_t y, uint32_t z, uint32_t w)
+    {
+        wout[(size_t)q4 * a.nr] = make_uint4(x, y, z, w);
+    }
+    __device__ void group_start(uint32_t g)
+    {
+        const size_t gi = (size_t)jb * GPS + g;
+#pragma unroll
+        for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = cnt[w][tid];
+    }
+    __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * GPS + g) * a.nr + r] = sum; }
+};
+
+__global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
+{
+    __shared__ LogEntry s_log[LOG_TAB];
+    __shared__ PickEntry s_pick[PICK_TAB];
+    __shared__ uint32_t s_cnt[CNT_WORDS][256];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = a.tab.logt[i];
+    for (uint32_t i = tid; i < PICK_TAB; i += 256) s_pick[i] = a.tab.pick[i];
+#pragma unroll
+    for (uint32_t w = 0; w < CNT_WORDS; ++w) s_cnt[w][tid] = 0;
+    __syncthreads();
+
+    const uint32_t r = blockIdx.x * 256 + tid;  // slice-local run (< nr)
+    const uint32_t seg = blockIdx.y;
+    const uint64_t run = a.run_begin + r;
+    Rng ri = rng_seed(seed_interval(a.seed_base, run));
+    Rng rp = rng_seed(seed_picker(a.seed_base, run));
+    if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
+
+    const uint32_t b0 = seg * SEG;
+    DevCtx cx{a, s_cnt, tid, tid & 63u, r, seg, seg - a.band_lo, 0u, r < a.n,
+              reinterpret_cast<uint4 *>(a.words) + (size_t)(b0 >> 2) * a.nr + r};
+    const uint64_t tsum = draw_segment(cx, ri, rp, s_log, s_pick, b0, seg >= a.band_lo);
+    a.segsum[(size_t)seg * a.nr + r] = tsum;
+#pragma unroll
+    for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = s_cnt[w][tid];
+    a.nslow[(size_t)seg * a.nr + r] = cx.nsl;
+}
+
+__global__ void msim_interval_kernel(const LogEntry *__restrict__ lt, const uint64_t *__restrict__ u,
+                                     int64_t *__restrict__ out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool ok;
+    const int32_t q = interval_ms_fast(u[i], lt, ok);
+    out[i] = ok ? q : interval_ms_exact_dev(u[i]);
+}
+
+__global__ void msim_pick_kernel(const PickEntry *__restrict__ pt, const uint64_t *__restrict__ u,
+                                 int32_t *__restrict__ out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = pick_info(u[i], pt) & 15u;
+    out[i] = k == 15u ? -1 : (int32_t)k;
+}
+
+hipError_t launch_intervals(const LogEntry *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(msim_interval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lt, u, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_picks(const PickEntry *pt, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(msim_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pt, u, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_draws(const DrawArgs &a, hipStream_t s)
+{
+    hipLaunchKernelGGL(msim_draws_kernel, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace msim

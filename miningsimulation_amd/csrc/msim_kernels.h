@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "msim_dispatch.h"
+#include "msim_pipeline.h"
 
 namespace msim {
 
@@ -21,6 +22,9 @@ struct LaunchArgs {
     uint32_t err_cap;
     uint32_t *status;     // 2 u32 or null
     hipStream_t stream;
+    const PipeLayout *pl; // event-skipping pipeline layout (honest networks) or null (per-lane kernel)
+    char *pipe_ws;        // pipeline workspace (pl->total bytes)
+    PipeTables tab;       // device tables of the config on this device
 };
 
 hipError_t launch_runs(const LaunchArgs &a);
@@ -31,9 +35,11 @@ MSIM_FOR_EACH_M(MSIM_DECL_LAUNCH)
 hipError_t launch_finalize(const uint64_t *partials, uint32_t nparts, uint32_t nvals, uint64_t *out,
                            const uint32_t *retry_count, const uint32_t *fail_count, uint32_t retry_cap,
                            uint32_t *status, hipStream_t stream);
+hipError_t launch_draws(const DrawArgs &a, hipStream_t s);
 hipError_t launch_log1p(const double *x, double *out, uint64_t n, hipStream_t s);
-hipError_t launch_intervals(const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s);
-hipError_t launch_picks(const SimParams &p, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
+// Production draw paths of the pipeline (msim_fastdraw.h) over given uniforms (test/sampler surface).
+hipError_t launch_intervals(const LogEntry *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s);
+hipError_t launch_picks(const PickEntry *pt, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
 constexpr int TPB = 256;  // 4 waves of 64 lanes per workgroup
 size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap);
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "msim_kernels.h"
+#include "msim_pipeline.h"
 
 namespace msim {
 
@@ -85,7 +86,137 @@ __global__ __launch_bounds__(TPB) void msim_runs_kernel(const SimParams p, const
     block_reduce_store<M>(v, partials + (size_t)blockIdx.x * 6 * M);
 }
 
+// ------------------------------------------------------------------ event-skipping pipeline (K2, K3)
+// K2: one lane per listed non-fast block (msim_pipeline.h episode_entry).
+template <int M>
+__global__ __launch_bounds__(TPB) void msim_episode_kernel(const SimParams p, const PipeArgs a)
+{
+    const uint32_t cnt = *a.list_count;
+    const uint32_t lim = cnt < a.lcap ? cnt : a.lcap;
+    for (uint32_t idx = blockIdx.x * TPB + threadIdx.x; idx < lim; idx += gridDim.x * TPB) episode_entry<M>(p, a, idx);
+}
+
+// K3: one lane per run (msim_pipeline.h combine_run), then the MinerStats reduction.
+template <int M>
+__global__ __launch_bounds__(TPB) void msim_combine_kernel(const SimParams p, const PipeArgs a, const uint32_t n,
+                                                          const uint32_t rel_begin, uint64_t *__restrict__ partials,
+                                                          uint32_t *__restrict__ records, uint32_t *__restrict__ best_h,
+                                                          uint32_t *__restrict__ err_count, uint32_t *__restrict__ err_list,
+                                                          const uint32_t err_cap)
+{
+    const uint32_t r = blockIdx.x * TPB + threadIdx.x;
+    const bool active = r < n;
+    uint32_t F[M], S[M];
+    const bool ok = active ? combine_run<M>(p, a, r, F, S) : false;
+    uint64_t v[6 * M];
+#pragma unroll
+    for (int i = 0; i < 6 * M; ++i) v[i] = 0;
+    if (active && !ok) {
+        const uint32_t pos = atomicAdd(err_count, 1u);
+        if (pos < err_cap) err_list[pos] = rel_begin + r;
+    } else if (active) {
+        uint32_t L = 0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) L += F[k];  // sum of found = |best chain| - 1
+        const uint32_t rel = rel_begin + r;
+        const double Ld = (double)L;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            const uint32_t f = F[k];
+            // MinerStats (main.cpp:28-29)
+            const double share = f == 0 ? 0.0 : (double)f / Ld;
+            const double rate = f == 0 ? 0.0 : (double)S[k] / (double)f;
+            const uint64_t sfx = (uint64_t)(share * 4294967296.0 + 0.5);
+            const uint64_t rfx = (uint64_t)(rate * 4294967296.0 + 0.5);
+            v[6 * k + 0] = f;
+            v[6 * k + 1] = S[k];
+            v[6 * k + 2] = sfx >> 32;
+            v[6 * k + 3] = sfx & 0xFFFFFFFFull;
+            v[6 * k + 4] = rfx >> 32;
+            v[6 * k + 5] = rfx & 0xFFFFFFFFull;
+            if (records) {
+                records[2 * ((size_t)rel * M + k) + 0] = f;
+                records[2 * ((size_t)rel * M + k) + 1] = S[k];
+            }
+        }
+        if (best_h) best_h[rel] = L;
+    }
+    block_reduce_store<M>(v, partials + (size_t)blockIdx.x * 6 * M);
+}
+
 // ------------------------------------------------------------------ host-side launch table
+template <int M>
+static void launch_retry(const LaunchArgs &a, uint64_t *parts_retry, uint32_t nbr)
+{
+    if (a.p.selfish >= 0)
+        hipLaunchKernelGGL((msim_runs_kernel<M, true, true, NX_WIDE, NG_WIDE, true>), dim3(nbr), dim3(TPB), 0, a.stream,
+                           a.p, a.run_begin, a.n, a.seed_base, a.err_list, a.err_count, a.err_cap, parts_retry, a.records,
+                           a.best_h, a.fail_count, nullptr, 0u);
+    else
+        hipLaunchKernelGGL((msim_runs_kernel<M, false, true, NX_WIDE, NG_WIDE, true>), dim3(nbr), dim3(TPB), 0, a.stream,
+                           a.p, a.run_begin, a.n, a.seed_base, a.err_list, a.err_count, a.err_cap, parts_retry, a.records,
+                           a.best_h, a.fail_count, nullptr, 0u);
+}
+
+// Event-skipping pipeline (msim_pipeline.h), slice by slice on the caller's stream.
+template <int M>
+static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
+{
+    const PipeLayout &L = *a.pl;
+    char *ws = a.pipe_ws;
+    PipeArgs pa;
+    pa.nr = L.nr;
+    pa.nseg = L.nseg;
+    pa.nb = L.nb;
+    pa.cap = L.cap;
+    pa.band_lo = L.band_lo;
+    pa.lcap = L.lcap;
+    pa.rec_words = L.rec_words;
+    pa.words = (const uint32_t *)(ws + L.words_off);
+    pa.segsum = (const uint64_t *)(ws + L.segsum_off);
+    pa.segcnt = (const uint32_t *)(ws + L.segcnt_off);
+    pa.nslow = (const uint32_t *)(ws + L.nslow_off);
+    pa.slots = (const uint32_t *)(ws + L.slots_off);
+    pa.gsum = (const uint32_t *)(ws + L.gsum_off);
+    pa.gcum = (const uint32_t *)(ws + L.gcum_off);
+    pa.list = (const EpEntry *)(ws + L.list_off);
+    pa.list_count = (const uint32_t *)(ws + L.count_off);
+    pa.recs = (uint32_t *)(ws + L.recs_off);
+    DrawArgs da;
+    da.tab = a.tab;
+    da.seed_base = a.seed_base;
+    da.nr = L.nr;
+    da.nseg = L.nseg;
+    da.cap = L.cap;
+    da.band_lo = L.band_lo;
+    da.lcap = L.lcap;
+    da.words = (uint32_t *)(ws + L.words_off);
+    da.segsum = (uint64_t *)(ws + L.segsum_off);
+    da.segcnt = (uint32_t *)(ws + L.segcnt_off);
+    da.nslow = (uint32_t *)(ws + L.nslow_off);
+    da.slots = (uint32_t *)(ws + L.slots_off);
+    da.gsum = (uint32_t *)(ws + L.gsum_off);
+    da.gcum = (uint32_t *)(ws + L.gcum_off);
+    da.list = (EpEntry *)(ws + L.list_off);
+    da.list_count = (uint32_t *)(ws + L.count_off);
+    uint32_t ep_grid = (L.lcap + TPB - 1) / TPB;
+    if (ep_grid > 8192) ep_grid = 8192;
+    if (ep_grid == 0) ep_grid = 1;
+    for (uint32_t off = 0; off < a.n; off += L.nr) {
+        const uint32_t cn = (a.n - off) < L.nr ? (a.n - off) : L.nr;
+        if (hipMemsetAsync(da.list_count, 0, sizeof(uint32_t), a.stream) != hipSuccess) return hipErrorUnknown;
+        da.run_begin = a.run_begin + off;
+        da.n = cn;
+        hipError_t e = launch_draws(da, a.stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((msim_episode_kernel<M>), dim3(ep_grid), dim3(TPB), 0, a.stream, a.p, pa);
+        hipLaunchKernelGGL((msim_combine_kernel<M>), dim3((cn + TPB - 1) / TPB), dim3(TPB), 0, a.stream, a.p, pa, cn,
+                           off, parts + (size_t)(off / TPB) * 6 * M, a.records, a.best_h, a.err_count, a.err_list,
+                           a.err_cap);
+    }
+    return hipGetLastError();
+}
+
 template <int M>
 static hipError_t launch_m(const LaunchArgs &a)
 {
@@ -94,7 +225,10 @@ static hipError_t launch_m(const LaunchArgs &a)
     const bool self = a.p.selfish >= 0;
     uint64_t *parts = a.partials;
     uint64_t *parts_retry = a.partials + (size_t)nb * 6 * M;
-    if (nb) {
+    if (a.pl) {
+        const hipError_t e = launch_pipeline<M>(a, parts);
+        if (e != hipSuccess) return e;
+    } else if (nb) {
         if (self)
             hipLaunchKernelGGL((msim_runs_kernel<M, true, true, NX_FAST, NG_FAST, false>), dim3(nb), dim3(TPB), 0, a.stream,
                                a.p, a.run_begin, a.n, a.seed_base, nullptr, nullptr, 0u, parts, a.records, a.best_h,
@@ -104,16 +238,9 @@ static hipError_t launch_m(const LaunchArgs &a)
                                a.p, a.run_begin, a.n, a.seed_base, nullptr, nullptr, 0u, parts, a.records, a.best_h,
                                a.err_count, a.err_list, a.err_cap);
     }
-    // Retry kernel: wider capacities and deep branches for every run the fast kernel flagged. Its
-    // grid is fixed (err_cap lanes); lanes beyond the device-side count exit at once.
-    if (self)
-        hipLaunchKernelGGL((msim_runs_kernel<M, true, true, NX_WIDE, NG_WIDE, true>), dim3(nbr), dim3(TPB), 0, a.stream,
-                           a.p, a.run_begin, a.n, a.seed_base, a.err_list, a.err_count, a.err_cap, parts_retry, a.records,
-                           a.best_h, a.fail_count, nullptr, 0u);
-    else
-        hipLaunchKernelGGL((msim_runs_kernel<M, false, true, NX_WIDE, NG_WIDE, true>), dim3(nbr), dim3(TPB), 0, a.stream,
-                           a.p, a.run_begin, a.n, a.seed_base, a.err_list, a.err_count, a.err_cap, parts_retry, a.records,
-                           a.best_h, a.fail_count, nullptr, 0u);
+    // Retry kernel: wider capacities and deep branches for every run flagged above. Its grid is fixed
+    // (err_cap lanes); lanes beyond the device-side count exit at once.
+    launch_retry<M>(a, parts_retry, nbr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_finalize(a.partials, nb + nbr, (uint32_t)(6 * M), a.sums, a.err_count, a.fail_count, a.err_cap,

@@ -42,6 +42,20 @@ enum : uint32_t {
     ERR_EXTRA = 2u,   // too many simultaneously in-flight honest blocks
     ERR_GROUPS = 4u,  // too many in-flight reveal groups
     ERR_PICK = 8u,    // PickFinder fell through its table (simulation.h:220 assert)
+    ERR_DRAWS = 16u,  // an episode ran past the pre-generated draws of its run
+};
+
+// Outcome of one episode (Sim::episode): the run's state machine started from a quiet state at
+// block `start` and ran until it was quiet again (end = next unconsumed block) or until the end of
+// the run (ended). F are per-owner block-count DELTAS: +1 per episode block in the chain, -1 per
+// block consumed (modular u32; see msim_pipeline.h for how they combine).
+template <int M>
+struct EpisodeOut {
+    uint32_t F[M];
+    uint32_t S[M];  // stale_blocks increments (simulation.h:133)
+    uint32_t end;
+    uint32_t ended;
+    uint32_t err;
 };
 
 struct SimParams {
@@ -496,6 +510,93 @@ struct Sim {
         }
         out.best_height = wb + (uint32_t)bl;
         out.err = err;
+    }
+
+    // All chains identical and published, nothing withheld or in flight (caller checked ea == T_INF).
+    MSIM_HD bool is_quiet() const
+    {
+        if (DEEP && deep) return false;
+        if (SELF && (w != 0 || ng != 0)) return false;
+        bool q = true;
+#pragma unroll
+        for (int k = 1; k < M; ++k) q = q && rt[k] == rt[0] && str[k] == str[0];
+#pragma unroll
+        for (int k = 0; k < M; ++k) q = q && rp[k] == rt[k];
+        return q;
+    }
+
+    // One episode of RunSimulation (main.cpp:150-182) that starts in the quiet state at the find of
+    // block `src.index` (time T0) and stops at the first event after which the network is quiet
+    // again, or at the end of the run (then it also evaluates main.cpp:185-189 like run()).
+    // Src: uint32_t word() = (I << 5 | fast << 4 | k) of the current block; bool advance(); index.
+    template <class Src>
+    MSIM_HD void episode(const SimParams &p, Src &src, int64_t T0, EpisodeOut<M> &out)
+    {
+        init();
+        const int sidx = SELF ? p.selfish : -1;
+        const int64_t D = p.duration_ms;
+        int64_t nbt = T0, t = T0;
+        bool quiet = false;
+        while (t < D && err == 0) {
+            while (t == nbt) {  // main.cpp:153-157
+                const int k = (int)(src.word() & 15u);
+                if (k >= M) {
+                    err |= ERR_PICK;
+                    break;
+                }
+                found_block(k, t, p);
+#pragma unroll
+                for (int kk = 0; kk < M; ++kk) F[kk] -= (kk == k) ? 1u : 0u;  // consumed (re-added by the caller)
+                if (!src.advance()) {
+                    err |= ERR_DRAWS;
+                    break;
+                }
+                nbt += (int64_t)(src.word() >> 5);
+            }
+            if (err) break;
+            publish(t, sidx);
+            int bj;
+            int32_t bl;
+            int64_t ba;
+            uint64_t bs;
+            bool bb;
+            best(bj, bl, ba, bs, bb);
+            notify(t, bl, ba, bs, bb, p);
+            bpub = bl;
+            if (bl >= FOLD_AT) fold(sidx);
+            const int64_t ea = earliest_arrival(t, sidx);
+            if (ea == T_INF && is_quiet()) {
+                quiet = true;
+                break;
+            }
+            t = lmin(nbt, ea);
+        }
+        out.err = err;
+        out.end = src.index;
+        out.ended = quiet ? 0u : 1u;
+        if (err) return;
+        if (quiet) {
+            const uint64_t r = nib_upto(rt[0]);
+#pragma unroll
+            for (int k = 0; k < M; ++k) out.F[k] = F[k] + (uint32_t)count_nib(str[0], (uint32_t)k, r);
+        } else {
+            publish(D, sidx);  // main.cpp:185: BestChain at the end of the run, no notify
+            int bj;
+            int32_t bl;
+            int64_t ba;
+            uint64_t bs;
+            bool bb;
+            best(bj, bl, ba, bs, bb);
+            const uint64_t r = nib_upto(bl);
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+                uint32_t f = F[k] + (uint32_t)count_nib(bs, (uint32_t)k, r);
+                if (DEEP && deep) f += bb ? DB[k] : DA[k];
+                out.F[k] = f;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < M; ++k) out.S[k] = stl[k];
     }
 };
 

@@ -1,0 +1,373 @@
+// msim_pipeline.h — the event-skipping pipeline for honest networks.
+//
+// RunSimulation (/root/reference/main.cpp:128-192) spends almost every event in one state: all
+// chains identical and published ("quiet"). From a quiet state, a block i found at T_i by an honest
+// miner k whose successor comes later than its arrival (I_{i+1} > prop_k) is adopted by everyone at
+// T_i + prop_k and leaves the network quiet again — a "fast" block. Everything else is an EPISODE,
+// a pure function of the draws from its first block on (translation-invariant in time apart from the
+// end of the run). So one run is computed as
+//
+//   K1 msim_draws_kernel    (run, segment) workers, jump-ahead to draw j*SEG, produce every block's
+//                           word (interval, fast bit, finder), per-segment time and per-owner counts,
+//                           and append every non-fast block to a dense episode list;
+//   K2 msim_episode_kernel  one lane per listed block: the full state machine (msim_model.h) from a
+//                           quiet state at that block, until quiet again or the end of the run;
+//   K3 msim_combine_kernel  one lane per run: locate the end of the run (first T_i >= D), chain the
+//                           episodes that start from a quiet state, and combine
+//                              found_k = #{i < n_end : finder_i = k} + sum(episode deltas)
+//                           stale_k = sum(episode stale counts).
+// Runs that hit any capacity (draw budget, slots, list) are flagged and recomputed by the per-lane
+// retry kernel, so results never depend on these capacities.
+#pragma once
+#include <math.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "msim_fastdraw.h"
+#include "msim_model.h"
+
+namespace msim {
+
+constexpr uint32_t SEG = 2048;          // draws per K1 worker
+constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
+constexpr uint32_t GPS = SEG / GROUP;   // groups per segment
+constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pairs (<= 16 owners)
+
+struct EpEntry {
+    uint32_t run;     // slice-local run
+    uint32_t block;   // block index within the run
+    uint64_t offset;  // T_block - (start time of its segment), ms
+};
+
+struct PipeLayout {
+    uint32_t nr;       // runs in a slice (multiple of 256)
+    uint32_t nseg;     // segments per run
+    uint32_t nb;       // nseg * SEG pre-generated blocks per run
+    uint32_t cap;      // slow-block slots per (run, segment)
+    uint32_t band_lo;  // first segment with group metadata (where the run can end)
+    uint32_t nband;
+    uint32_t lcap;     // episode list capacity
+    uint32_t rec_words;
+    size_t words_off, segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gcum_off, list_off, recs_off,
+        count_off, total;
+};
+
+// Device tables (per config, per device): pick table, log table, jump matrices.
+struct PipeTables {
+    const PickEntry *pick;
+    const LogEntry *logt;
+    const uint32_t *jump;  // nseg * 128 columns of 4 words
+};
+
+struct DrawArgs {
+    PipeTables tab;
+    uint64_t run_begin;   // absolute index of the slice's first run
+    uint32_t n;           // valid runs in the slice
+    uint32_t seed_base;
+    uint32_t nr, nseg, cap, band_lo, lcap;
+    uint32_t *words;      // [nb/4][nr][4]
+    uint64_t *segsum;     // [nseg][nr]
+    uint32_t *segcnt;     // [nseg][8][nr]
+    uint32_t *nslow;      // [nseg][nr]
+    uint32_t *slots;      // [nseg][cap][nr]
+    uint32_t *gsum;       // [nband][GPS][nr]
+    uint32_t *gcum;       // [nband][GPS][8][nr]
+    EpEntry *list;        // [lcap]
+    uint32_t *list_count;
+};
+
+struct PipeArgs {  // K2 / K3
+    uint32_t nr, nseg, nb, cap, band_lo, lcap, rec_words;
+    const uint32_t *words;
+    const uint64_t *segsum;
+    const uint32_t *segcnt;
+    const uint32_t *nslow;
+    const uint32_t *slots;
+    const uint32_t *gsum;
+    const uint32_t *gcum;
+    const EpEntry *list;
+    const uint32_t *list_count;
+    uint32_t *recs;       // [lcap][rec_words]: end, flags, F[M], S[M]
+};
+
+enum : uint32_t { REC_ENDED = 1u, REC_ERR = 2u, REC_SKIP = 4u };
+
+MSIM_HD size_t word_index(uint32_t nr, uint32_t run, uint32_t block)
+{
+    return ((size_t)(block >> 2) * nr + run) * 4 + (block & 3u);
+}
+
+// Episode draw source: the words of one run, from a given block on.
+struct WordSrc {
+    const uint32_t *words;
+    uint32_t nr, nb, run, index;
+    uint32_t cur;
+    MSIM_HD uint32_t word() const { return cur; }
+    MSIM_HD bool advance()
+    {
+        if (index + 1 >= nb) return false;
+        ++index;
+        cur = words[word_index(nr, run, index)];
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------- sizing (host)
+// Every capacity has a >= 8-sigma margin; a run that exceeds one anyway is recomputed by the retry
+// kernel, so the sizes only affect speed, never results. rho = P(block is not fast).
+inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget)
+{
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    PipeLayout L;
+    const double D = (double)duration_ms;
+    const double mu = D / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
+    L.nseg = (uint32_t)ceil((mu + 12.0 * sd + 64.0) / SEG);
+    if (L.nseg < 1) L.nseg = 1;
+    L.nb = L.nseg * SEG;
+    const double lo = mu - 12.0 * sd - 64.0;
+    L.band_lo = lo > 0 ? (uint32_t)floor(lo / SEG) : 0u;
+    if (L.band_lo >= L.nseg) L.band_lo = L.nseg - 1;
+    L.nband = L.nseg - L.band_lo;
+    const double lam = rho * SEG;
+    L.cap = (uint32_t)ceil(lam + 8.0 * sqrt(lam) + 8.0);
+    L.rec_words = 2 + 2 * m;
+    const double per_run = (double)L.nb * 4 + L.nseg * (8.0 + CNT_WORDS * 4 + 4 + 4.0 * L.cap) +
+                           L.nband * GPS * (4.0 + CNT_WORDS * 4) + rho * L.nb * (sizeof(EpEntry) + 4.0 * L.rec_words);
+    uint64_t cap_runs = (uint64_t)(budget / per_run) / 256 * 256;
+    if (cap_runs < 256) cap_runs = 256;
+    const uint64_t want = (n_runs + 255) / 256 * 256;
+    L.nr = (uint32_t)(want < cap_runs ? want : cap_runs);
+    const double ent = (double)L.nr * rho * L.nb;
+    L.lcap = (uint32_t)ceil(ent + 8.0 * sqrt(ent) + 1024.0);
+    size_t o = 0;
+    L.words_off = o;
+    o = al(o + (size_t)L.nb * L.nr * 4);
+    L.segsum_off = o;
+    o = al(o + (size_t)L.nseg * L.nr * 8);
+    L.segcnt_off = o;
+    o = al(o + (size_t)L.nseg * CNT_WORDS * L.nr * 4);
+    L.nslow_off = o;
+    o = al(o + (size_t)L.nseg * L.nr * 4);
+    L.slots_off = o;
+    o = al(o + (size_t)L.nseg * L.cap * L.nr * 4);
+    L.gsum_off = o;
+    o = al(o + (size_t)L.nband * GPS * L.nr * 4);
+    L.gcum_off = o;
+    o = al(o + (size_t)L.nband * GPS * CNT_WORDS * L.nr * 4);
+    L.list_off = o;
+    o = al(o + (size_t)L.lcap * sizeof(EpEntry));
+    L.recs_off = o;
+    o = al(o + (size_t)L.lcap * L.rec_words * 4);
+    L.count_off = o;
+    o = al(o + 4);
+    L.total = o;
+    return L;
+}
+
+// ---------------------------------------------------------------- K1 lane body (shared host/device)
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u);
+#endif
+
+MSIM_HD uint32_t draw_interval(Rng &ri, const LogEntry *__restrict__ lt)
+{
+    const uint64_t u = rng_next(ri);
+    bool ok;
+    const int32_t q = interval_ms_fast(u, lt, ok);
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)(ok ? q : interval_ms_exact_dev(u));
+#else
+    return (uint32_t)(ok ? q : (int32_t)interval_ms_of(u));
+#endif
+}
+
+// One (run, segment) worker: SEG blocks from the jumped RNG states. Ctx supplies the side effects:
+//   count(k)                per-owner counter of this lane (+1 for owner k)
+//   snapshot(w)             packed counter word w (u16 pairs)
+//   slow(block, offset)     a non-fast block (offset = its find time minus the segment's start)
+//   store4(q4, a, b, c, d)  words of blocks 4*q4 .. 4*q4+3 of the segment
+//   group(g, sum)           band only: sum of the group's intervals
+//   group_start(g)          band only: called before group g's first block (snapshot the counters)
+template <class Ctx>
+MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogEntry *__restrict__ lt,
+                              const PickEntry *__restrict__ pt, uint32_t b0, bool band)
+{
+    uint32_t Icur = draw_interval(ri, lt);
+    uint32_t infocur = pick_info(rng_next(rp), pt);
+    uint64_t tsum = 0;
+    uint32_t gacc = 0;
+    for (uint32_t q4 = 0; q4 < SEG / 4; ++q4) {
+        if (band && (q4 & 7u) == 0) cx.group_start(q4 >> 3);
+        uint32_t wv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t Inext = draw_interval(ri, lt);  // I_{i+1}
+            const uint32_t infonext = pick_info(rng_next(rp), pt);
+            tsum += Icur;
+            gacc += Icur;
+            const uint32_t k = infocur & 15u;
+            const bool fast = Inext > (infocur >> 4);
+            wv[q] = (Icur << 5) | (fast ? 16u : 0u) | k;
+            cx.count(k);
+            cx.slow(!fast, b0 + q4 * 4 + (uint32_t)q, tsum);
+            Icur = Inext;
+            infocur = infonext;
+        }
+        cx.store4(q4, wv[0], wv[1], wv[2], wv[3]);
+        if (band && (q4 & 7u) == 7u) {
+            cx.group(q4 >> 3, gacc);
+            gacc = 0;
+        }
+    }
+    return tsum;
+}
+
+// ---------------------------------------------------------------- K3 lane body (shared host/device)
+template <int M>
+MSIM_HD void add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, size_t stride)
+{
+#pragma unroll
+    for (int w = 0; w < (M + 1) / 2; ++w) {
+        const uint32_t c = src[(size_t)w * stride];
+        F[2 * w] += c & 0xFFFFu;
+        if (2 * w + 1 < M) F[2 * w + 1] += c >> 16;
+    }
+}
+
+// Combine one run r of a slice. Returns false when the run must be recomputed by the retry path.
+template <int M>
+MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M])
+{
+    const int64_t D = p.duration_ms;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        F[k] = 0;
+        S[k] = 0;
+    }
+    // 1. Segment containing the end of the run: the first whose last block is found at >= D.
+    int64_t T = 0;
+    int e = -1;
+    for (uint32_t j = 0; j < a.nseg; ++j) {
+        const int64_t ss = (int64_t)a.segsum[(size_t)j * a.nr + r];
+        if (T + ss >= D) {
+            e = (int)j;
+            break;
+        }
+        T += ss;
+        add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr);
+    }
+    if (e < (int)a.band_lo) return false;  // past the pre-generated draws or outside the band
+    // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153).
+    const size_t gb = (size_t)(e - (int)a.band_lo) * GPS;
+    uint32_t G = GPS;
+    for (uint32_t g = 0; g < GPS; ++g) {
+        const int64_t gs = (int64_t)a.gsum[(gb + g) * a.nr + r];
+        if (T + gs >= D) {
+            G = g;
+            break;
+        }
+        T += gs;
+    }
+    if (G == GPS) return false;
+    add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr);
+    const uint32_t bg = (uint32_t)e * SEG + G * GROUP;
+    uint32_t n_end = 0;
+    int64_t t_last = 0;
+    bool done = false;
+#pragma unroll 4
+    for (uint32_t q = 0; q < GROUP; ++q) {
+        const uint32_t wd = a.words[word_index(a.nr, r, bg + q)];
+        if (!done) {
+            const int64_t Tn = T + (int64_t)(wd >> 5);
+            if (Tn >= D) {
+                done = true;
+                n_end = bg + q;
+                t_last = T;
+            } else {
+                T = Tn;
+                const uint32_t k = wd & 15u;
+#pragma unroll
+                for (int kk = 0; kk < M; ++kk) F[kk] += (k == (uint32_t)kk) ? 1u : 0u;
+            }
+        }
+    }
+    if (!done) return false;
+    // 3. Episodes in block order; an episode applies when its first block is reached quiet.
+    uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
+    bool stop = false;
+    for (int j = 0; j <= e && !stop; ++j) {
+        const uint32_t ns = a.nslow[(size_t)j * a.nr + r];
+        if (ns > a.cap) return false;
+        for (uint32_t c = 0; c < ns; ++c) {
+            const uint32_t idx = a.slots[((size_t)j * a.cap + c) * a.nr + r];
+            if (idx >= a.lcap) return false;
+            const uint32_t s = a.list[idx].block;
+            if (s >= n_end) {  // no later episode starts before the end of the run
+                stop = true;
+                break;
+            }
+            if (s < cursor) continue;  // consumed by the previous episode
+            const uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
+            const uint32_t fl = rec[1];
+            if (fl & (REC_ERR | REC_SKIP)) return false;
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+                F[k] += rec[2 + k];
+                S[k] += rec[2 + M + k];
+            }
+            cursor = rec[0];
+            if (fl & REC_ENDED) {  // the run ended inside this episode
+                cursor = 0xFFFFFFFFu;
+                stop = true;
+                break;
+            }
+        }
+    }
+    // 4. The run ended quiet and its last block was a fast one: it counts only if it arrived by D.
+    if (cursor != 0xFFFFFFFFu && n_end > 0 && cursor < n_end) {
+        const uint32_t k = a.words[word_index(a.nr, r, n_end - 1)] & 15u;
+        int64_t pk = 0;
+#pragma unroll
+        for (int kk = 0; kk < M; ++kk)
+            if ((uint32_t)kk == k) pk = p.prop[kk];
+        if (t_last + pk > D) {
+#pragma unroll
+            for (int kk = 0; kk < M; ++kk) F[kk] -= ((uint32_t)kk == k) ? 1u : 0u;
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- K2 lane body (shared host/device)
+template <int M>
+MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
+{
+    const EpEntry e = a.list[idx];
+    uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
+    const uint32_t seg = e.block / SEG;
+    int64_t T = (int64_t)e.offset;
+    for (uint32_t j = 0; j < seg; ++j) T += (int64_t)a.segsum[(size_t)j * a.nr + e.run];
+    if (T >= p.duration_ms) {  // beyond the end of the run: never applied
+        rec[1] = REC_SKIP;
+        return;
+    }
+    WordSrc src;
+    src.words = a.words;
+    src.nr = a.nr;
+    src.nb = a.nb;
+    src.run = e.run;
+    src.index = e.block;
+    src.cur = a.words[word_index(a.nr, e.run, e.block)];
+    Sim<M, false, true, NX_WIDE, NG_WIDE> s;
+    EpisodeOut<M> o;
+    s.episode(p, src, T, o);
+    rec[0] = o.end;
+    rec[1] = (o.ended ? REC_ENDED : 0u) | (o.err ? REC_ERR : 0u);
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        rec[2 + k] = o.F[k];
+        rec[2 + M + k] = o.S[k];
+    }
+}
+
+}  // namespace msim

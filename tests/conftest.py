@@ -32,10 +32,11 @@ def native_tests():
     import __graft_entry__ as ge
 
     lib = os.path.join(ROOT, "build", "libmodel_host.so")
+    pipe = os.path.join(ROOT, "build", "libpipeline_host.so")
     chk = os.path.join(ROOT, "build", "draws_check")
-    if not (os.path.exists(lib) and os.path.exists(chk)):
+    if not (os.path.exists(lib) and os.path.exists(chk) and os.path.exists(pipe)):
         ge.build_native_tests()
-    return {"model_host": lib, "draws_check": chk}
+    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe}
 
 
 @pytest.fixture(scope="session")

@@ -10,6 +10,9 @@
 #include <string.h>
 
 #include "../../miningsimulation_amd/csrc/msim_draws.h"
+#include "../../miningsimulation_amd/csrc/msim_fastdraw.h"
+
+static msim::LogEntry g_log[msim::LOG_TAB];
 
 static int64_t ref_interval(uint64_t u)
 {
@@ -19,8 +22,40 @@ static int64_t ref_interval(uint64_t u)
 }
 
 struct Job {
-    uint64_t n, seed, bad_log1p, bad_interval, first_bad_u;
+    uint64_t n, seed, bad_log1p, bad_interval, first_bad_u, bad_fast, fallbacks;
+    double max_err_ns;  // |fast 6e11*E + 0.5 - (fl(6e11*E_glibc) + 0.5)|
 };
+
+// The draw kernel's fast interval (msim_fastdraw.h) with its exact fallback, vs the reference.
+static void check_fast(uint64_t u, Job *j)
+{
+    bool ok;
+    const int32_t q = msim::interval_ms_fast(u, g_log, ok);
+    const int64_t fast = ok ? (int64_t)q : msim::interval_ms_of(u);
+    if (!ok) j->fallbacks++;
+    if (fast != ref_interval(u)) {
+        j->bad_fast++;
+        if (!j->first_bad_u) j->first_bad_u = u;
+    }
+    // error of the approximation itself (before the margin test)
+    const double e = -log1p((double)(u >> 11) * -0x1.0p-53);
+    const double yref = msim::BLOCK_INTERVAL_NS * e + 0.5;
+    const uint64_t n = (1ull << 53) - (u >> 11);
+    const int lz = __builtin_clzll(n);
+    const uint64_t nn = n << lz;
+    const int jj = (int)((nn >> 56) & 127);
+    const double w = __builtin_bit_cast(double, (0x3FFull << 52) | ((nn >> 11) & 0xFFFFFFFFFFFFFull));
+    const double r = fma(w, g_log[jj].invc, -1.0);
+    double p = fma(r, 0.2, -0.25);
+    p = fma(r, p, 1.0 / 3.0);
+    p = fma(r, p, -0.5);
+    p = fma(r * r, p, r);
+    const double ed = (double)(10 - lz);
+    const double lo = fma(ed, 1.90821492927058770002e-10, g_log[jj].L + p);
+    const double z = fma(-msim::BLOCK_INTERVAL_NS, fma(ed, 6.93147180369123816490e-01, lo), 0.5);
+    const double err = fabs(z - yref);
+    if (err > j->max_err_ns) j->max_err_ns = err;
+}
 
 static int check_one(uint64_t u, Job *j)
 {
@@ -36,7 +71,76 @@ static int check_one(uint64_t u, Job *j)
         bad = 1;
     }
     if (bad && !j->first_bad_u) j->first_bad_u = u;
+    check_fast(u, j);
     return bad;
+}
+
+// PickFinder (simulation.h:213-221) by its linear scan vs the draw kernel's table lookup.
+static uint64_t check_picks(uint64_t seed)
+{
+    msim::Rng r = msim::rng_seed(seed);
+    uint64_t bad = 0;
+    for (int cfg = 0; cfg < 400; ++cfg) {
+        const int m = 1 + (int)(msim::rng_next(r) % 15);
+        uint64_t perc[15] = {0};
+        int64_t prop[15] = {0};
+        uint8_t self[15] = {0};
+        int left = 100;
+        for (int k = 0; k < m - 1; ++k) {
+            perc[k] = msim::rng_next(r) % (uint64_t)(left + 1);
+            left -= (int)perc[k];
+        }
+        perc[m - 1] = (uint64_t)left;
+        for (int k = 0; k < m; ++k) prop[k] = (int64_t)(msim::rng_next(r) % 40000);
+        msim::PickEntry tab[msim::PICK_TAB];
+        msim::build_pick_table(perc, prop, self, m, tab);
+        auto scan = [&](uint64_t u) {
+            uint64_t i = 0;
+            for (int k = 0; k < m; ++k) {
+                i += perc[k] * msim::PERC_MULTIPLIER;
+                if (i > u) return k;
+            }
+            return 15;
+        };
+        auto test = [&](uint64_t u) {
+            const uint32_t info = msim::pick_info(u, tab);
+            const int k = (int)(info & 15u);
+            const uint32_t fthr = info >> 4;
+            const uint32_t want_thr = k < 15 ? (uint32_t)prop[k] : msim::FTHR_NEVER;
+            if (k != scan(u) || fthr != want_thr) bad++;
+        };
+        for (int i = 0; i < 20000; ++i) test(msim::rng_next(r));
+        for (uint64_t c = 0; c <= 100; ++c) {
+            const uint64_t t = c * msim::PERC_MULTIPLIER;
+            for (int64_t d = -3; d <= 3; ++d) test(t + (uint64_t)d);
+        }
+        test(~0ull);
+        test(~0ull - 15);
+        test(~0ull - 16);
+    }
+    return bad;
+}
+
+// Inputs whose 6e11*E + 0.5 lies within a few ns of a millisecond boundary (the fallback's domain).
+static void near_boundaries(Job *j, uint64_t *count)
+{
+    msim::Rng r = msim::rng_seed(99);
+    for (int i = 0; i < 200000; ++i) {
+        const double qms = (double)(msim::rng_next(r) % 22000000ull);
+        const double off = ((double)(int64_t)(msim::rng_next(r) % 8001) - 4000.0) * 1e-3;  // +-4 ns
+        const double y = qms * 1e6 - 0.5 + off;
+        if (y <= 0) continue;
+        const double v = exp(-y / msim::BLOCK_INTERVAL_NS);
+        const double m = (1.0 - v) * 0x1.0p53;
+        if (!(m >= 0 && m < 9007199254740991.0)) continue;
+        const uint64_t mb = (uint64_t)m;
+        for (int64_t d = -2; d <= 2; ++d) {
+            const uint64_t mm = mb + (uint64_t)d;
+            if (mm >= (1ull << 53)) continue;
+            check_one((mm << 11) | (msim::rng_next(r) & 0x7FF), j);
+            (*count)++;
+        }
+    }
 }
 
 static void *worker(void *p)
@@ -51,6 +155,7 @@ int main(int argc, char **argv)
 {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 10000000ull;
     const int th = argc > 2 ? atoi(argv[2]) : 8;
+    msim::build_log_table(g_log);
     Job *jobs = (Job *)calloc((size_t)th, sizeof(Job));
     pthread_t *t = (pthread_t *)calloc((size_t)th, sizeof(pthread_t));
     for (int i = 0; i < th; ++i) {
@@ -58,11 +163,15 @@ int main(int argc, char **argv)
         jobs[i].seed = 0x51ed5eedull + (uint64_t)i;
         pthread_create(&t[i], nullptr, worker, &jobs[i]);
     }
-    uint64_t bl = 0, bi = 0, first = 0, total = 0;
+    uint64_t bl = 0, bi = 0, first = 0, total = 0, bf = 0, fb = 0;
+    double maxerr = 0;
     for (int i = 0; i < th; ++i) {
         pthread_join(t[i], nullptr);
         bl += jobs[i].bad_log1p;
         bi += jobs[i].bad_interval;
+        bf += jobs[i].bad_fast;
+        fb += jobs[i].fallbacks;
+        if (jobs[i].max_err_ns > maxerr) maxerr = jobs[i].max_err_ns;
         total += jobs[i].n;
         if (!first) first = jobs[i].first_bad_u;
     }
@@ -88,8 +197,16 @@ int main(int argc, char **argv)
             check_one(q << 11, &s);
             structured++;
         }
-    printf("{\"random\": %llu, \"structured\": %llu, \"bad_log1p\": %llu, \"bad_interval\": %llu, \"first_bad_u\": %llu}\n",
-           (unsigned long long)total, (unsigned long long)structured, (unsigned long long)(bl + s.bad_log1p),
-           (unsigned long long)(bi + s.bad_interval), (unsigned long long)(first ? first : s.first_bad_u));
-    return (bl + bi + s.bad_log1p + s.bad_interval) ? 1 : 0;
+    uint64_t nb = 0;
+    near_boundaries(&s, &nb);
+    const uint64_t bp = check_picks(4242);
+    if (s.max_err_ns > maxerr) maxerr = s.max_err_ns;
+    printf("{\"random\": %llu, \"structured\": %llu, \"near_boundary\": %llu, \"bad_log1p\": %llu, "
+           "\"bad_interval\": %llu, \"bad_fast_interval\": %llu, \"fast_fallbacks\": %llu, \"fast_max_err_ns\": %.6g, "
+           "\"bad_picks\": %llu, \"first_bad_u\": %llu}\n",
+           (unsigned long long)total, (unsigned long long)structured, (unsigned long long)nb,
+           (unsigned long long)(bl + s.bad_log1p), (unsigned long long)(bi + s.bad_interval),
+           (unsigned long long)(bf + s.bad_fast), (unsigned long long)(fb + s.fallbacks), maxerr,
+           (unsigned long long)bp, (unsigned long long)(first ? first : s.first_bad_u));
+    return (bl + bi + bf + bp + s.bad_log1p + s.bad_interval + s.bad_fast) ? 1 : 0;
 }

@@ -46,7 +46,13 @@ def test_gpu_log1p_and_intervals(msim, oracle):
     # plus both ends of the domain and the branch thresholds of the fdlibm algorithm
     edge = np.concatenate([np.arange(4096, dtype=np.uint64) << np.uint64(11),
                            ((np.uint64(2**53 - 1) - np.arange(4096, dtype=np.uint64)) << np.uint64(11))])
-    u = np.concatenate([u, edge])
+    # and inputs whose 6e11*E + 0.5 lies within +-4 ns of a millisecond boundary: the domain of the
+    # draw kernel's exact fallback (msim_fastdraw.h)
+    q = rng.integers(1, 22_000_000, size=200_000).astype(np.float64)
+    y = q * 1e6 - 0.5 + rng.uniform(-4.0, 4.0, size=q.size)
+    m = ((1.0 - np.exp(-y / 6e11)) * 2.0**53).astype(np.uint64)
+    near = np.concatenate([m + np.uint64(d) for d in (0, 1, 2)]) << np.uint64(11)
+    u = np.concatenate([u, edge, near])
     x = (u >> np.uint64(11)).astype(np.float64) * -(2.0**-53)
     du = torch.from_numpy(u.view(np.int64)).cuda()
     dx = torch.from_numpy(x).cuda()
@@ -175,6 +181,19 @@ def test_gpu_sharding_is_exact(msim):
     for k in range(9):
         for fld in ("blocks_found", "stale_blocks", "share_hi", "share_lo", "rate_hi", "rate_lo"):
             assert getattr(whole.sums[k], fld) == getattr(a.sums[k], fld) + getattr(b.sums[k], fld)
+
+
+@pytest.mark.parametrize("preset", ["c1", "c2"])
+def test_gpu_pipeline_equals_per_lane_kernel(msim, preset, monkeypatch):
+    """The event-skipping pipeline (honest networks) and the per-lane kernel are two independent device
+    implementations of RunSimulation: 4096 runs, per-run counters must be identical."""
+    miners = msim.PRESETS[preset]()
+    fast = msim.Simulation(miners).run(4096, 77_000, 1000, 0, per_run=True)
+    monkeypatch.setenv("MSIM_NO_PIPELINE", "1")
+    slow = msim.Simulation(miners).run(4096, 77_000, 1000, 0, per_run=True)
+    assert np.array_equal(fast.found, slow.found)
+    assert np.array_equal(fast.stale, slow.stale)
+    assert np.array_equal(fast.best_height, slow.best_height)
 
 
 def test_gpu_invariants_full_scale(msim):
