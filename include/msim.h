@@ -106,6 +106,25 @@ int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t
 int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t *d_out_index, uint64_t n,
                       void *stream);
 
+/* Stage timing for measurement (bench.py): while enabled, every msim_launch records HIP events on its
+ * stream around the whole launch and around each draw kernel (K1, the dominant kernel of the
+ * event-skipping pipeline). msim_timing_read synchronises on those events, returns the summed
+ * elapsed milliseconds and the number of launches since the last enable/read, and clears them. */
+int msim_timing_enable(int on);
+int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches);
+
+/* How msim_launch will execute n_runs of this config on the current device. */
+typedef struct msim_pipeline_layout {
+    uint32_t uses_pipeline;   /* 1: event-skipping pipeline (honest network); 0: per-lane kernel */
+    uint32_t slice_runs;      /* runs per pipeline slice */
+    uint32_t segment_blocks;  /* blocks per draw-kernel worker */
+    uint32_t segments;        /* workers per run */
+    uint64_t blocks_per_run;  /* pre-generated blocks per run (segments * segment_blocks) */
+    uint64_t workspace_bytes; /* pipeline part of msim_workspace_bytes */
+    double rho;               /* probability that a block starts a fork episode */
+} msim_pipeline_layout;
+int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_layout *out);
+
 /* Convert fixed-point sums to MinerStats-style doubles. */
 void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out);
 

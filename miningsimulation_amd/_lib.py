@@ -34,6 +34,9 @@ EXPORTED = (
     "msim_device_intervals",
     "msim_device_picks",
     "msim_sums_to_stats",
+    "msim_timing_enable",
+    "msim_timing_read",
+    "msim_pipeline_info",
     "msim_strerror",
     "msim_version",
 )
@@ -65,6 +68,18 @@ class MsimSums(ctypes.Structure):
 
 class MsimRunRecord(ctypes.Structure):
     _fields_ = [("found", ctypes.c_uint32), ("stale", ctypes.c_uint32)]
+
+
+class MsimPipelineLayout(ctypes.Structure):
+    _fields_ = [
+        ("uses_pipeline", ctypes.c_uint32),
+        ("slice_runs", ctypes.c_uint32),
+        ("segment_blocks", ctypes.c_uint32),
+        ("segments", ctypes.c_uint32),
+        ("blocks_per_run", ctypes.c_uint64),
+        ("workspace_bytes", ctypes.c_uint64),
+        ("rho", ctypes.c_double),
+    ]
 
 
 class MsimError(RuntimeError):
@@ -102,6 +117,13 @@ def _load() -> ctypes.CDLL:
     lib.msim_device_picks.restype = ctypes.c_int
     lib.msim_sums_to_stats.argtypes = [ctypes.POINTER(MsimSums), u32, ctypes.POINTER(MsimStats)]
     lib.msim_sums_to_stats.restype = None
+    lib.msim_timing_enable.argtypes = [ctypes.c_int]
+    lib.msim_timing_enable.restype = ctypes.c_int
+    lib.msim_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(u32)]
+    lib.msim_timing_read.restype = ctypes.c_int
+    lib.msim_pipeline_info.argtypes = [vp, u64, ctypes.POINTER(MsimPipelineLayout)]
+    lib.msim_pipeline_info.restype = ctypes.c_int
     lib.msim_strerror.argtypes = [ctypes.c_int]
     lib.msim_strerror.restype = ctypes.c_char_p
     lib.msim_version.argtypes = []

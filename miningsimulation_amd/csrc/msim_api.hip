@@ -30,7 +30,12 @@ struct msim_config {
     double rho;      // probability that a block is not "fast" (msim_pipeline.h)
     bool pipe_ok;    // event-skipping pipeline eligible (honest network, rare forks)
     std::mutex mu;
-    void *tables[MAX_DEVICES];  // per-device pipeline tables (lazily uploaded)
+    struct Tab {
+        int dev;
+        uint32_t seg, nseg;
+        void *ptr;
+    };
+    std::vector<Tab> tables;  // per (device, segment length) pipeline tables, lazily uploaded
 };
 
 namespace {
@@ -63,38 +68,71 @@ constexpr uint64_t MAX_LAUNCH_RUNS = 1ull << 26;
 constexpr double PIPE_MAX_RHO = 0.08;           // above this the per-lane kernel is cheaper
 constexpr double PIPE_SLICE_BUDGET = 16.0 * (1ull << 30);  // pipeline workspace per slice (bytes)
 
-msim::PipeLayout pipe_layout(const msim_config *c, uint64_t n_runs)
+// K1 wave slots of the current device (CUs x resident K1 waves per CU); 8192 if it cannot be queried.
+uint32_t draw_slots()
 {
-    return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET);
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        msim::draws_blocks_per_cu(&blocks) != hipSuccess || cus <= 0 || blocks <= 0)
+        return 8192;
+    return (uint32_t)(cus * blocks * 4);
 }
 
-// Pipeline tables for this config on the current device: pick table, log table, jump matrices.
-int device_tables(msim_config *c, uint32_t nseg, msim::PipeTables *out)
+msim::PipeLayout pipe_layout(const msim_config *c, uint64_t n_runs)
+{
+    return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET, draw_slots());
+}
+
+// Pipeline tables for this config on the current device: pick table, log table, jump matrices for
+// draw offsets j * seg.
+int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables *out)
 {
     using namespace msim;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) return MSIM_E_HIP;
+    if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
     std::lock_guard<std::mutex> g(c->mu);
     const size_t pick_b = PICK_TAB * sizeof(PickEntry), log_b = LOG_TAB * sizeof(LogEntry);
-    if (!c->tables[dev]) {
+    void *d = nullptr;
+    for (const auto &t : c->tables)
+        if (t.dev == dev && t.seg == seg && t.nseg >= nseg) d = t.ptr;
+    if (!d) {
         const size_t jump_b = (size_t)nseg * 128 * 16;
         std::vector<char> h(pick_b + log_b + jump_b);
         build_pick_table(c->perc, c->prop, c->self, (int)c->n, (PickEntry *)h.data());
         build_log_table((LogEntry *)(h.data() + pick_b));
-        build_jump_table(nseg, SEG, (uint32_t *)(h.data() + pick_b + log_b));
-        void *d = nullptr;
+        build_jump_table(nseg, seg, (uint32_t *)(h.data() + pick_b + log_b));
         if (hipMalloc(&d, h.size()) != hipSuccess) return MSIM_E_HIP;
         if (hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(d);
             return MSIM_E_HIP;
         }
-        c->tables[dev] = d;
+        c->tables.push_back({dev, seg, nseg, d});
     }
-    const char *d = (const char *)c->tables[dev];
-    out->pick = (const PickEntry *)d;
-    out->logt = (const LogEntry *)(d + pick_b);
-    out->jump = (const uint32_t *)(d + pick_b + log_b);
+    const char *b = (const char *)d;
+    out->pick = (const PickEntry *)b;
+    out->logt = (const LogEntry *)(b + pick_b);
+    out->jump = (const uint32_t *)(b + pick_b + log_b);
     return MSIM_OK;
+}
+
+// Stage timing (msim_timing_enable / msim_timing_read): HIP events recorded on the launch stream.
+struct Timing {
+    std::mutex mu;
+    bool on = false;
+    std::vector<hipEvent_t> k1;      // (begin, end) pairs around K1
+    std::vector<hipEvent_t> launch;  // (begin, end) pairs around msim_launch
+    uint32_t launches = 0;
+};
+Timing &timing()
+{
+    static Timing t;
+    return t;
+}
+
+void destroy_events(std::vector<hipEvent_t> &v)
+{
+    for (auto e : v) (void)hipEventDestroy(e);
+    v.clear();
 }
 
 // Process-wide log table (msim_fastdraw.h) per device, for msim_device_intervals.
@@ -163,7 +201,6 @@ int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms
     }
     c->rho = rho;
     c->pipe_ok = c->p.selfish < 0 && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
-    for (int d = 0; d < MAX_DEVICES; ++d) c->tables[d] = nullptr;
     *out = c;
     return MSIM_OK;
 }
@@ -171,8 +208,7 @@ int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms
 void msim_config_destroy(msim_config *cfg)
 {
     if (!cfg) return;
-    for (int d = 0; d < MAX_DEVICES; ++d)
-        if (cfg->tables[d]) (void)hipFree(cfg->tables[d]);
+    for (const auto &t : cfg->tables) (void)hipFree(t.ptr);
     delete cfg;
 }
 
@@ -216,13 +252,30 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
     a.stream = s;
     a.pl = nullptr;
     a.pipe_ws = nullptr;
+    a.k1_events = nullptr;
     if (cfg->pipe_ok) {
-        const int rc = device_tables(const_cast<msim_config *>(cfg), pl.nseg, &a.tab);
+        const int rc = device_tables(const_cast<msim_config *>(cfg), pl.seg, pl.nseg, &a.tab);
         if (rc) return rc;
         a.pl = &pl;
         a.pipe_ws = ws + l.total;
     }
-    return msim::launch_runs(a) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+    Timing &tm = timing();
+    std::unique_lock<std::mutex> lk(tm.mu);
+    hipEvent_t lb = nullptr, le = nullptr;
+    if (tm.on) {
+        a.k1_events = &tm.k1;
+        if (hipEventCreate(&lb) == hipSuccess && hipEventCreate(&le) == hipSuccess) {
+            tm.launch.push_back(lb);
+            tm.launch.push_back(le);
+            (void)hipEventRecord(lb, s);
+        }
+        tm.launches++;
+    } else {
+        lk.unlock();
+    }
+    const int rc = msim::launch_runs(a) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+    if (le) (void)hipEventRecord(le, s);
+    return rc;
 }
 
 int msim_device_log1p(const double *d_x, double *d_out, uint64_t n, void *stream)
@@ -244,7 +297,8 @@ int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t
 {
     if (!cfg || !d_uniform || !d_out_index) return MSIM_E_INVALID;
     msim::PipeTables t;
-    const int rc = device_tables(const_cast<msim_config *>(cfg), pipe_layout(cfg, 1).nseg, &t);
+    const msim::PipeLayout pl = pipe_layout(cfg, 1);
+    const int rc = device_tables(const_cast<msim_config *>(cfg), pl.seg, pl.nseg, &t);
     if (rc) return rc;
     return msim::launch_picks(t.pick, d_uniform, d_out_index, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
 }
@@ -331,6 +385,58 @@ out:
     (void)hipFree(rec);
     (void)hipFree(bh);
     return rc;
+}
+
+int msim_timing_enable(int on)
+{
+    Timing &tm = timing();
+    std::lock_guard<std::mutex> g(tm.mu);
+    destroy_events(tm.k1);
+    destroy_events(tm.launch);
+    tm.launches = 0;
+    tm.on = on != 0;
+    return MSIM_OK;
+}
+
+int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches)
+{
+    if (!draws_ms || !launch_ms || !launches) return MSIM_E_INVALID;
+    Timing &tm = timing();
+    std::lock_guard<std::mutex> g(tm.mu);
+    double d = 0, l = 0;
+    int rc = MSIM_OK;
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<hipEvent_t> &v = pass ? tm.launch : tm.k1;
+        for (size_t i = 0; i + 1 < v.size(); i += 2) {
+            float ms = 0;
+            if (hipEventSynchronize(v[i + 1]) != hipSuccess || hipEventElapsedTime(&ms, v[i], v[i + 1]) != hipSuccess)
+                rc = MSIM_E_HIP;
+            (pass ? l : d) += ms;
+        }
+    }
+    *draws_ms = d;
+    *launch_ms = l;
+    *launches = tm.launches;
+    destroy_events(tm.k1);
+    destroy_events(tm.launch);
+    tm.launches = 0;
+    return rc;
+}
+
+int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_layout *out)
+{
+    if (!cfg || !out || n_runs == 0) return MSIM_E_INVALID;
+    memset(out, 0, sizeof(*out));
+    out->rho = cfg->rho;
+    if (!cfg->pipe_ok) return MSIM_OK;
+    const msim::PipeLayout pl = pipe_layout(cfg, n_runs);
+    out->uses_pipeline = 1;
+    out->slice_runs = pl.nr;
+    out->segment_blocks = pl.seg;
+    out->segments = pl.nseg;
+    out->blocks_per_run = pl.nb;
+    out->workspace_bytes = pl.total;
+    return MSIM_OK;
 }
 
 const char *msim_strerror(int code)

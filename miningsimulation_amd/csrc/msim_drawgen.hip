@@ -81,14 +81,21 @@ struct DevCtx {
     }
     __device__ void group_start(uint32_t g)
     {
-        const size_t gi = (size_t)jb * GPS + g;
+        const size_t gi = (size_t)jb * a.gps + g;
 #pragma unroll
         for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = cnt[w][tid];
     }
-    __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * GPS + g) * a.nr + r] = sum; }
+    __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * a.gps + g) * a.nr + r] = sum; }
 };
 
+#ifndef MSIM_K1_WAVES
+#define MSIM_K1_WAVES 0
+#endif
+#if MSIM_K1_WAVES
+__global__ __launch_bounds__(256, MSIM_K1_WAVES) void msim_draws_kernel(const DrawArgs a)
+#else
 __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
+#endif
 {
     __shared__ LogEntry s_log[LOG_TAB];
     __shared__ PickEntry s_pick[PICK_TAB];
@@ -107,10 +114,10 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     Rng rp = rng_seed(seed_picker(a.seed_base, run));
     if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
 
-    const uint32_t b0 = seg * SEG;
+    const uint32_t b0 = seg * a.seg;
     DevCtx cx{a, s_cnt, tid, tid & 63u, r, seg, seg - a.band_lo, 0u, r < a.n,
               reinterpret_cast<uint4 *>(a.words) + (size_t)(b0 >> 2) * a.nr + r};
-    const uint64_t tsum = draw_segment(cx, ri, rp, s_log, s_pick, b0, seg >= a.band_lo);
+    const uint64_t tsum = draw_segment(cx, ri, rp, s_log, s_pick, b0, a.seg, seg >= a.band_lo);
     a.segsum[(size_t)seg * a.nr + r] = tsum;
 #pragma unroll
     for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = s_cnt[w][tid];
@@ -148,6 +155,11 @@ hipError_t launch_picks(const PickEntry *pt, const uint64_t *u, int32_t *out, ui
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(msim_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pt, u, out, n);
     return hipGetLastError();
+}
+
+hipError_t draws_blocks_per_cu(int *blocks)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_draws_kernel, 256, 0);
 }
 
 hipError_t launch_draws(const DrawArgs &a, hipStream_t s)

@@ -50,7 +50,26 @@ MSIM_HD Rng rng_seed(uint64_t seed)  // xoroshiro128++.h:23-24
     return r;
 }
 
-MSIM_HD uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+// 64-bit rotate; on gfx950 two 32-bit funnel shifts (v_alignbit_b32) per rotate instead of a 64-bit
+// shift pair (k is a compile-time constant at every call site).
+MSIM_HD uint64_t rotl64(uint64_t x, int k)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (k >= 32) {
+        const uint32_t t = lo;
+        lo = hi;
+        hi = t;
+        k -= 32;
+    }
+    if (k == 0) return ((uint64_t)hi << 32) | lo;
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - k);
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - k);
+    return ((uint64_t)nhi << 32) | nlo;
+#else
+    return (x << k) | (x >> (64 - k));
+#endif
+}
 
 MSIM_HD uint64_t rng_next(Rng &r)  // xoroshiro128++.h:26-34
 {

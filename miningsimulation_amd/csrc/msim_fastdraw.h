@@ -4,8 +4,8 @@
 //     ms = trunc(llround(6e11 * -log1p(-(u>>11) * 2^-53)) / 1e6)
 // with glibc's log1p. Only the millisecond value matters, and it changes only where 6e11*E + 0.5
 // crosses a multiple of 1e6. So the fast path evaluates E with a cheap table method (128-entry
-// 1/c table, degree-5 log1p polynomial, FMAs allowed) whose total error against glibc's bits is
-// < 0.02 ns in 6e11*E, and accepts its result only when 6e11*E + 0.5 lies at least
+// 1/c table, degree-4 log1p polynomial, FMAs allowed) whose total error against glibc's bits is
+// < 0.2 ns in 6e11*E, and accepts its result only when 6e11*E + 0.5 lies at least
 // MARGIN_NS = 1 ns away from every millisecond boundary; anything closer (2e-6 of draws) is recomputed
 // by the bit-exact glibc sequence of msim_draws.h. The result is therefore identical to the
 // reference's for every input, not just statistically.
@@ -27,11 +27,12 @@ constexpr int PICK_TAB = 100;
 constexpr double MARGIN_NS = 1.0;
 constexpr uint32_t FTHR_NEVER = (1u << 27) - 1;  // > any interval (max 22 044 720 ms < 2^25)
 
+// Table entry j (w in [1 + j/128, 1 + (j+1)/128)): invc ~ 1/c_j, c_j = 1 + (j + 1/2)/128, and
+// A = (0.5 - 6e11 * log(1/invc)) * 1e-6: the entry's share of z = (6e11*E + 0.5) / 1e6 in ms.
 struct LogEntry {
-    double invc;  // ~1/c_j, c_j = 1 + (j + 1/2)/128
-    double L;     // -log(invc) = log(1/invc), correctly rounded from an 80-bit evaluation
+    double invc;
+    double A;
 };
-
 // Pick table entry for p1 = floor(100u/2^64): info for p = p1 (lo) and p = p1 + 1 (hi).
 // info = k | fthr << 4: k = finder (15 = fell through, simulation.h:220), fthr = the interval that
 // the NEXT draw must exceed for the block to be "fast" (honest finder, next find after arrival).
@@ -41,7 +42,12 @@ struct PickEntry {
 };
 
 // Fast interval with exactness check; on `ok == false` the caller must use the exact path.
-MSIM_HD int32_t interval_ms_fast(uint64_t u, const LogEntry *__restrict__ tab, bool &ok)
+// z = (6e11 * E + 0.5) / 1e6 = A_j - 6e5 * (e*ln2 + log1p(r)), E = -log(v), v = 2^e * w, r = w*invc - 1;
+// log1p(r) by a degree-4 polynomial (|r| <= 2^-8: truncation <= 2e-13, i.e. 0.11 ns in 6e11*E).
+// The reference's interval is floor(z) whenever frac(z) is at least MARGIN_NS/1e6 from 0 and 1.
+constexpr double FD_C1 = -6e5, FD_C2 = 3e5, FD_C3 = -2e5, FD_C4 = 1.5e5;  // -6e5 * (1, -1/2, 1/3, -1/4)
+constexpr double FD_CE = -6e5 * 6.93147180559945309417e-01;              // -6e5 * ln 2
+MSIM_HD double interval_fast_z(uint64_t u, const LogEntry *__restrict__ tab)
 {
     const uint64_t n = (1ull << 53) - (u >> 11);  // 2^53 * (1 + x), exact, in [1, 2^53]
     const int lz = __builtin_clzll(n);
@@ -51,18 +57,23 @@ MSIM_HD int32_t interval_ms_fast(uint64_t u, const LogEntry *__restrict__ tab, b
     const double w = __builtin_bit_cast(double, (0x3FFull << 52) | ((nn >> 11) & 0xFFFFFFFFFFFFFull));
     const LogEntry t = tab[j];
     const double r = __builtin_fma(w, t.invc, -1.0);
-    double p = __builtin_fma(r, 0.2, -0.25);
-    p = __builtin_fma(r, p, 1.0 / 3.0);
-    p = __builtin_fma(r, p, -0.5);
-    p = __builtin_fma(r * r, p, r);
-    const double ed = (double)e;
-    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-    const double lo = __builtin_fma(ed, ln2_lo, t.L + p);
-    const double logv = __builtin_fma(ed, ln2_hi, lo);
-    const double z = __builtin_fma(-BLOCK_INTERVAL_NS, logv, 0.5);  // 6e11*E + 0.5
-    const int32_t q = (int32_t)(z * 1e-6);
-    const double rem = __builtin_fma(-(double)q, 1e6, z);
-    ok = (rem >= MARGIN_NS) && (rem <= 1e6 - MARGIN_NS);
+    double p = __builtin_fma(r, FD_C4, FD_C3);
+    p = __builtin_fma(r, p, FD_C2);
+    p = __builtin_fma(r, p, FD_C1);
+    p = r * p;                                    // -6e5 * log1p(r)
+    return __builtin_fma((double)e, FD_CE, t.A + p);
+}
+
+MSIM_HD int32_t interval_ms_fast(uint64_t u, const LogEntry *__restrict__ tab, bool &ok)
+{
+    const double z = interval_fast_z(u, tab);
+    const int32_t q = (int32_t)z;                 // z >= 0.5e-6 > 0: truncation = floor
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double f = __builtin_amdgcn_fract(z);
+#else
+    const double f = z - (double)q;
+#endif
+    ok = (f >= MARGIN_NS * 1e-6) && (f <= 1.0 - MARGIN_NS * 1e-6);
     return q;
 }
 
@@ -84,7 +95,8 @@ inline void build_log_table(LogEntry *out)
         const double c = 1.0 + (j + 0.5) / LOG_TAB;
         const double invc = 1.0 / c;
         out[j].invc = invc;
-        out[j].L = (double)(-logl((long double)invc));
+        const long double L = -logl((long double)invc);  // log(1/invc), 80-bit
+        out[j].A = (double)((0.5L - 6e11L * L) * 1e-6L);
     }
 }
 

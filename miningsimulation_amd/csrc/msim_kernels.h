@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "msim_dispatch.h"
 #include "msim_pipeline.h"
 
@@ -25,6 +27,7 @@ struct LaunchArgs {
     const PipeLayout *pl; // event-skipping pipeline layout (honest networks) or null (per-lane kernel)
     char *pipe_ws;        // pipeline workspace (pl->total bytes)
     PipeTables tab;       // device tables of the config on this device
+    std::vector<hipEvent_t> *k1_events;  // stage timing: (begin, end) pairs around every K1, or null
 };
 
 hipError_t launch_runs(const LaunchArgs &a);
@@ -36,6 +39,7 @@ hipError_t launch_finalize(const uint64_t *partials, uint32_t nparts, uint32_t n
                            const uint32_t *retry_count, const uint32_t *fail_count, uint32_t retry_cap,
                            uint32_t *status, hipStream_t stream);
 hipError_t launch_draws(const DrawArgs &a, hipStream_t s);
+hipError_t draws_blocks_per_cu(int *blocks);  // resident K1 workgroups per CU
 hipError_t launch_log1p(const double *x, double *out, uint64_t n, hipStream_t s);
 // Production draw paths of the pipeline (msim_fastdraw.h) over given uniforms (test/sampler surface).
 hipError_t launch_intervals(const LogEntry *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s);

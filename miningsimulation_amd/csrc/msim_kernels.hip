@@ -166,6 +166,8 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     char *ws = a.pipe_ws;
     PipeArgs pa;
     pa.nr = L.nr;
+    pa.seg = L.seg;
+    pa.gps = L.gps;
     pa.nseg = L.nseg;
     pa.nb = L.nb;
     pa.cap = L.cap;
@@ -186,6 +188,8 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.tab = a.tab;
     da.seed_base = a.seed_base;
     da.nr = L.nr;
+    da.seg = L.seg;
+    da.gps = L.gps;
     da.nseg = L.nseg;
     da.cap = L.cap;
     da.band_lo = L.band_lo;
@@ -207,7 +211,14 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
         if (hipMemsetAsync(da.list_count, 0, sizeof(uint32_t), a.stream) != hipSuccess) return hipErrorUnknown;
         da.run_begin = a.run_begin + off;
         da.n = cn;
+        hipEvent_t eb = nullptr, ee = nullptr;
+        if (a.k1_events && hipEventCreate(&eb) == hipSuccess && hipEventCreate(&ee) == hipSuccess) {
+            a.k1_events->push_back(eb);
+            a.k1_events->push_back(ee);
+            (void)hipEventRecord(eb, a.stream);
+        }
         hipError_t e = launch_draws(da, a.stream);
+        if (ee) (void)hipEventRecord(ee, a.stream);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((msim_episode_kernel<M>), dim3(ep_grid), dim3(TPB), 0, a.stream, a.p, pa);
         hipLaunchKernelGGL((msim_combine_kernel<M>), dim3((cn + TPB - 1) / TPB), dim3(TPB), 0, a.stream, a.p, pa, cn,

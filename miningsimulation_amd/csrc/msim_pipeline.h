@@ -28,9 +28,8 @@
 
 namespace msim {
 
-constexpr uint32_t SEG = 2048;          // draws per K1 worker
 constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
-constexpr uint32_t GPS = SEG / GROUP;   // groups per segment
+constexpr uint32_t MIN_SEG = 512;       // shortest K1 worker (keeps the jump-ahead cost < 5 %)
 constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pairs (<= 16 owners)
 
 struct EpEntry {
@@ -41,8 +40,10 @@ struct EpEntry {
 
 struct PipeLayout {
     uint32_t nr;       // runs in a slice (multiple of 256)
-    uint32_t nseg;     // segments per run
-    uint32_t nb;       // nseg * SEG pre-generated blocks per run
+    uint32_t seg;      // blocks per K1 worker (multiple of GROUP)
+    uint32_t gps;      // groups per segment (seg / GROUP)
+    uint32_t nseg;     // segments (K1 workers) per run
+    uint32_t nb;       // nseg * seg pre-generated blocks per run
     uint32_t cap;      // slow-block slots per (run, segment)
     uint32_t band_lo;  // first segment with group metadata (where the run can end)
     uint32_t nband;
@@ -64,20 +65,20 @@ struct DrawArgs {
     uint64_t run_begin;   // absolute index of the slice's first run
     uint32_t n;           // valid runs in the slice
     uint32_t seed_base;
-    uint32_t nr, nseg, cap, band_lo, lcap;
+    uint32_t nr, seg, gps, nseg, cap, band_lo, lcap;
     uint32_t *words;      // [nb/4][nr][4]
     uint64_t *segsum;     // [nseg][nr]
     uint32_t *segcnt;     // [nseg][8][nr]
     uint32_t *nslow;      // [nseg][nr]
     uint32_t *slots;      // [nseg][cap][nr]
-    uint32_t *gsum;       // [nband][GPS][nr]
-    uint32_t *gcum;       // [nband][GPS][8][nr]
+    uint32_t *gsum;       // [nband][gps][nr]
+    uint32_t *gcum;       // [nband][gps][8][nr]
     EpEntry *list;        // [lcap]
     uint32_t *list_count;
 };
 
 struct PipeArgs {  // K2 / K3
-    uint32_t nr, nseg, nb, cap, band_lo, lcap, rec_words;
+    uint32_t nr, seg, gps, nseg, nb, cap, band_lo, lcap, rec_words;
     const uint32_t *words;
     const uint64_t *segsum;
     const uint32_t *segcnt;
@@ -115,28 +116,52 @@ struct WordSrc {
 // ---------------------------------------------------------------- sizing (host)
 // Every capacity has a >= 8-sigma margin; a run that exceeds one anyway is recomputed by the retry
 // kernel, so the sizes only affect speed, never results. rho = P(block is not fast).
-inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget)
+// `slots` = wave slots of K1 on the device (CUs x resident waves per CU). The run is cut into `nseg`
+// workers of `seg` blocks so that the K1 grid fills the device in whole rounds: every wave does the
+// same work, so a partial last round would leave SIMDs idle.
+inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget,
+                                  uint32_t slots)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     PipeLayout L;
     const double D = (double)duration_ms;
     const double mu = D / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
-    L.nseg = (uint32_t)ceil((mu + 12.0 * sd + 64.0) / SEG);
-    if (L.nseg < 1) L.nseg = 1;
-    L.nb = L.nseg * SEG;
-    const double lo = mu - 12.0 * sd - 64.0;
-    L.band_lo = lo > 0 ? (uint32_t)floor(lo / SEG) : 0u;
-    if (L.band_lo >= L.nseg) L.band_lo = L.nseg - 1;
-    L.nband = L.nseg - L.band_lo;
-    const double lam = rho * SEG;
-    L.cap = (uint32_t)ceil(lam + 8.0 * sqrt(lam) + 8.0);
+    const double need = mu + 8.0 * sd + 64.0;  // blocks to pre-generate (P(more) < 1e-15 per run)
+    const uint64_t want = (n_runs + 255) / 256 * 256;
+    // slice size first (memory), with an upper estimate of the per-run bytes
     L.rec_words = 2 + 2 * m;
-    const double per_run = (double)L.nb * 4 + L.nseg * (8.0 + CNT_WORDS * 4 + 4 + 4.0 * L.cap) +
-                           L.nband * GPS * (4.0 + CNT_WORDS * 4) + rho * L.nb * (sizeof(EpEntry) + 4.0 * L.rec_words);
+    const double nb_est = need + 2.0 * MIN_SEG;
+    const double per_run = nb_est * 4.0 + 64.0 * (8.0 + CNT_WORDS * 4 + 4) + 4.0 * (rho * nb_est * 2 + 64.0 * 16) +
+                           2.0 * nb_est / GROUP * (4.0 + CNT_WORDS * 4) + rho * nb_est * (sizeof(EpEntry) + 4.0 * L.rec_words);
     uint64_t cap_runs = (uint64_t)(budget / per_run) / 256 * 256;
     if (cap_runs < 256) cap_runs = 256;
-    const uint64_t want = (n_runs + 255) / 256 * 256;
     L.nr = (uint32_t)(want < cap_runs ? want : cap_runs);
+    // workers per run: minimise rounds(w) * (seg(w) + jump cost), jump ~ 25 blocks of work
+    const double rows = L.nr / 64.0;
+    if (slots < 1) slots = 1;
+    uint32_t best_w = 1;
+    double best_f = 1e300;
+    for (uint32_t w = 1; w <= 256; ++w) {
+        const uint32_t sg = (uint32_t)ceil(need / w / GROUP) * GROUP;
+        if (sg < MIN_SEG && w > 1) break;
+        const double rounds = ceil(rows * w / slots);
+        const double f = rounds * (sg + 25.0);
+        if (f < best_f * 0.999) {
+            best_f = f;
+            best_w = w;
+        }
+    }
+    L.nseg = best_w;
+    L.seg = (uint32_t)ceil(need / best_w / GROUP) * GROUP;
+    if (L.seg < GROUP) L.seg = GROUP;
+    L.gps = L.seg / GROUP;
+    L.nb = L.nseg * L.seg;
+    const double lo = mu - 8.0 * sd - 64.0;
+    L.band_lo = lo > 0 ? (uint32_t)floor(lo / L.seg) : 0u;
+    if (L.band_lo >= L.nseg) L.band_lo = L.nseg - 1;
+    L.nband = L.nseg - L.band_lo;
+    const double lam = rho * L.seg;
+    L.cap = (uint32_t)ceil(lam + 8.0 * sqrt(lam) + 8.0);
     const double ent = (double)L.nr * rho * L.nb;
     L.lcap = (uint32_t)ceil(ent + 8.0 * sqrt(ent) + 1024.0);
     size_t o = 0;
@@ -151,9 +176,9 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     L.slots_off = o;
     o = al(o + (size_t)L.nseg * L.cap * L.nr * 4);
     L.gsum_off = o;
-    o = al(o + (size_t)L.nband * GPS * L.nr * 4);
+    o = al(o + (size_t)L.nband * L.gps * L.nr * 4);
     L.gcum_off = o;
-    o = al(o + (size_t)L.nband * GPS * CNT_WORDS * L.nr * 4);
+    o = al(o + (size_t)L.nband * L.gps * CNT_WORDS * L.nr * 4);
     L.list_off = o;
     o = al(o + (size_t)L.lcap * sizeof(EpEntry));
     L.recs_off = o;
@@ -190,13 +215,13 @@ MSIM_HD uint32_t draw_interval(Rng &ri, const LogEntry *__restrict__ lt)
 //   group_start(g)          band only: called before group g's first block (snapshot the counters)
 template <class Ctx>
 MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogEntry *__restrict__ lt,
-                              const PickEntry *__restrict__ pt, uint32_t b0, bool band)
+                              const PickEntry *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
 {
     uint32_t Icur = draw_interval(ri, lt);
     uint32_t infocur = pick_info(rng_next(rp), pt);
     uint64_t tsum = 0;
     uint32_t gacc = 0;
-    for (uint32_t q4 = 0; q4 < SEG / 4; ++q4) {
+    for (uint32_t q4 = 0; q4 < seg / 4; ++q4) {
         if (band && (q4 & 7u) == 0) cx.group_start(q4 >> 3);
         uint32_t wv[4];
 #pragma unroll
@@ -258,9 +283,9 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     }
     if (e < (int)a.band_lo) return false;  // past the pre-generated draws or outside the band
     // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153).
-    const size_t gb = (size_t)(e - (int)a.band_lo) * GPS;
-    uint32_t G = GPS;
-    for (uint32_t g = 0; g < GPS; ++g) {
+    const size_t gb = (size_t)(e - (int)a.band_lo) * a.gps;
+    uint32_t G = a.gps;
+    for (uint32_t g = 0; g < a.gps; ++g) {
         const int64_t gs = (int64_t)a.gsum[(gb + g) * a.nr + r];
         if (T + gs >= D) {
             G = g;
@@ -268,9 +293,9 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         }
         T += gs;
     }
-    if (G == GPS) return false;
+    if (G == a.gps) return false;
     add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr);
-    const uint32_t bg = (uint32_t)e * SEG + G * GROUP;
+    const uint32_t bg = (uint32_t)e * a.seg + G * GROUP;
     uint32_t n_end = 0;
     int64_t t_last = 0;
     bool done = false;
@@ -344,7 +369,7 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
 {
     const EpEntry e = a.list[idx];
     uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
-    const uint32_t seg = e.block / SEG;
+    const uint32_t seg = e.block / a.seg;
     int64_t T = (int64_t)e.offset;
     for (uint32_t j = 0; j < seg; ++j) T += (int64_t)a.segsum[(size_t)j * a.nr + e.run];
     if (T >= p.duration_ms) {  // beyond the end of the run: never applied

@@ -33,7 +33,7 @@ struct HostCtx {
     }
     void store4(uint32_t q4, uint32_t x, uint32_t y, uint32_t z, uint32_t w)
     {
-        const uint32_t b = seg * SEG + q4 * 4;
+        const uint32_t b = seg * L.seg + q4 * 4;
         (*words)[word_index(L.nr, r, b)] = x;
         (*words)[word_index(L.nr, r, b + 1)] = y;
         (*words)[word_index(L.nr, r, b + 2)] = z;
@@ -41,17 +41,17 @@ struct HostCtx {
     }
     void group_start(uint32_t g)
     {
-        for (uint32_t w = 0; w < CNT_WORDS; ++w) (*gcum)[(((size_t)jb * GPS + g) * CNT_WORDS + w) * L.nr + r] = cnt[w];
+        for (uint32_t w = 0; w < CNT_WORDS; ++w) (*gcum)[(((size_t)jb * L.gps + g) * CNT_WORDS + w) * L.nr + r] = cnt[w];
     }
-    void group(uint32_t g, uint32_t sum) { (*gsum)[((size_t)jb * GPS + g) * L.nr + r] = sum; }
+    void group(uint32_t g, uint32_t sum) { (*gsum)[((size_t)jb * L.gps + g) * L.nr + r] = sum; }
 };
 
 template <int M>
 int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, const uint8_t *self, double rho,
-                 uint32_t seed_base, uint64_t run_begin, uint32_t n, uint32_t cap_override, uint32_t *found,
+                 uint32_t seed_base, uint64_t run_begin, uint32_t n, uint32_t cap_override, uint32_t wave_slots, uint32_t *found,
                  uint32_t *stale, uint8_t *ok, uint32_t *n_episodes)
 {
-    PipeLayout L = pipe_layout_for(rho, M, p.duration_ms, n, 1e18);
+    PipeLayout L = pipe_layout_for(rho, M, p.duration_ms, n, 1e18, wave_slots);
     L.nr = n;  // no padding on the host
     if (cap_override) L.cap = cap_override;
     L.lcap = 0xFFFFFFF0u;
@@ -60,10 +60,10 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     std::vector<uint32_t> jump((size_t)L.nseg * 128 * 4);
     build_pick_table(perc, prop, self, M, pick.data());
     build_log_table(logt.data());
-    build_jump_table(L.nseg, SEG, jump.data());
+    build_jump_table(L.nseg, L.seg, jump.data());
     std::vector<uint32_t> words((size_t)L.nb * n), segcnt((size_t)L.nseg * CNT_WORDS * n), nslow((size_t)L.nseg * n),
-        slots((size_t)L.nseg * L.cap * n, 0xFFFFFFFFu), gsum((size_t)L.nband * GPS * n),
-        gcum((size_t)L.nband * GPS * CNT_WORDS * n);
+        slots((size_t)L.nseg * L.cap * n, 0xFFFFFFFFu), gsum((size_t)L.nband * L.gps * n),
+        gcum((size_t)L.nband * L.gps * CNT_WORDS * n);
     std::vector<uint64_t> segsum((size_t)L.nseg * n);
     std::vector<EpEntry> list;
     for (uint32_t r = 0; r < n; ++r) {
@@ -81,7 +81,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
             mat_apply(m, si.s0, si.s1, ri.s0, ri.s1);
             mat_apply(m, sp.s0, sp.s1, rp.s0, rp.s1);
             if (ri.s0 != qi.s0 || ri.s1 != qi.s1 || rp.s0 != qp.s0 || rp.s1 != qp.s1) return -100;  // jump broken
-            for (uint32_t i = 0; i < SEG; ++i) {
+            for (uint32_t i = 0; i < L.seg; ++i) {
                 rng_next(qi);
                 rng_next(qp);
             }
@@ -95,7 +95,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
             cx.gsum = &gsum;
             cx.gcum = &gcum;
             cx.list = &list;
-            segsum[(size_t)j * n + r] = draw_segment(cx, ri, rp, logt.data(), pick.data(), j * SEG, j >= L.band_lo);
+            segsum[(size_t)j * n + r] = draw_segment(cx, ri, rp, logt.data(), pick.data(), j * L.seg, L.seg, j >= L.band_lo);
             for (uint32_t w = 0; w < CNT_WORDS; ++w) segcnt[((size_t)j * CNT_WORDS + w) * n + r] = cx.cnt[w];
             nslow[(size_t)j * n + r] = cx.nsl;
         }
@@ -104,6 +104,8 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     uint32_t count = (uint32_t)list.size();
     PipeArgs a;
     a.nr = n;
+    a.seg = L.seg;
+    a.gps = L.gps;
     a.nseg = L.nseg;
     a.nb = L.nb;
     a.cap = L.cap;
@@ -137,7 +139,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
 
 extern "C" int pipeline_run(const uint64_t *perc, const int64_t *prop, const uint8_t *selfish, int m,
                             int64_t duration_ms, uint32_t seed_base, uint64_t run_begin, uint32_t n,
-                            uint32_t cap_override, uint32_t *found, uint32_t *stale, uint8_t *ok,
+                            uint32_t cap_override, uint32_t wave_slots, uint32_t *found, uint32_t *stale, uint8_t *ok,
                             uint32_t *n_episodes)
 {
     SimParams p;
@@ -148,7 +150,7 @@ extern "C" int pipeline_run(const uint64_t *perc, const int64_t *prop, const uin
     for (int k = 0; k < m; ++k) rho += (double)perc[k] / 100.0 * (1.0 - exp(-((double)prop[k] + 1.0) / 599999.5));
 #define CASE(MM) \
     case MM:     \
-        return run_pipeline<MM>(p, perc, prop, selfish, rho, seed_base, run_begin, n, cap_override, found, stale, ok, n_episodes);
+        return run_pipeline<MM>(p, perc, prop, selfish, rho, seed_base, run_begin, n, cap_override, wave_slots, found, stale, ok, n_episodes);
     switch (m) { MSIM_FOR_EACH_M(CASE) default: return -1; }
 #undef CASE
 }

@@ -13,6 +13,6 @@ def test_log1p_and_interval_bit_exact(native_tests):
     # the draw kernel's fast interval (msim_fastdraw.h): identical results incl. ~1e6 inputs within
     # +-4 ns of a millisecond boundary; its raw error stays far inside the 1 ns acceptance margin
     assert res["bad_fast_interval"] == 0 and res["near_boundary"] > 900_000, res
-    assert res["fast_max_err_ns"] < 0.05, res
+    assert res["fast_max_err_ns"] < 0.25, res
     # PickFinder by table lookup == the reference's linear scan (random draws + every threshold +-3)
     assert res["bad_picks"] == 0, res

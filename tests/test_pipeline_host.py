@@ -18,7 +18,7 @@ H = [30, 29, 12, 11, 8, 5, 3, 1, 1]
 def pipe(native_tests):
     lib = ctypes.CDLL(native_tests["pipeline_host"])
 
-    def run(percs, props, duration, n, base=1000, begin=0, cap=0):
+    def run(percs, props, duration, n, base=1000, begin=0, cap=0, slots=8192):
         m = len(percs)
         f = (ctypes.c_uint32 * (n * m))()
         s = (ctypes.c_uint32 * (n * m))()
@@ -26,7 +26,7 @@ def pipe(native_tests):
         ne = ctypes.c_uint32()
         rc = lib.pipeline_run((ctypes.c_uint64 * m)(*percs), (ctypes.c_int64 * m)(*props), (ctypes.c_uint8 * m)(),
                               m, ctypes.c_int64(duration), ctypes.c_uint32(base), ctypes.c_uint64(begin),
-                              ctypes.c_uint32(n), ctypes.c_uint32(cap), f, s, ok, ctypes.byref(ne))
+                              ctypes.c_uint32(n), ctypes.c_uint32(cap), ctypes.c_uint32(slots), f, s, ok, ctypes.byref(ne))
         assert rc == 0, f"pipeline_run rc={rc} (-100: jump-ahead state differs from sequential stepping)"
         return (np.array(f, dtype=np.int64).reshape(n, m), np.array(s, dtype=np.int64).reshape(n, m),
                 np.array(ok, dtype=bool), ne.value)
@@ -34,8 +34,8 @@ def pipe(native_tests):
     return run
 
 
-def _check(pipe, oracle, percs, props, duration, n, base=1000, begin=0, cap=0, need_all_ok=True):
-    f, s, ok, ne = pipe(percs, props, duration, n, base, begin, cap)
+def _check(pipe, oracle, percs, props, duration, n, base=1000, begin=0, cap=0, need_all_ok=True, slots=8192):
+    f, s, ok, ne = pipe(percs, props, duration, n, base, begin, cap, slots)
     of, os_, _, _ = oracle.run_batch(percs, props, [0] * len(percs), duration, n, begin, base, threads=8)
     if need_all_ok:
         assert ok.all(), f"{(~ok).sum()} runs flagged for retry"
@@ -47,6 +47,12 @@ def _check(pipe, oracle, percs, props, duration, n, base=1000, begin=0, cap=0, n
 @pytest.mark.parametrize("prop", [0, 1, 100, 1000, 10_000, 30_000])
 def test_presets_full_year(pipe, oracle, prop):
     _check(pipe, oracle, H, [prop] * 9, D, 12)
+
+
+@pytest.mark.parametrize("slots", [1, 64, 5000, 10**6])
+def test_worker_geometries(pipe, oracle, slots):
+    """Segment lengths from one worker per run (no jump) to the shortest allowed workers."""
+    _check(pipe, oracle, H, [1000] * 9, D, 8, slots=slots)
 
 
 def _rand_percs(m, rng):
