@@ -21,6 +21,8 @@ from .simulation import (  # noqa: F401
     report,
     setup_miners,
     sums_to_stats,
+    timing_enable,
+    timing_read,
 )
 
 __version__ = "0.1.0"

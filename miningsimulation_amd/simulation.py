@@ -141,6 +141,12 @@ class Simulation:
             res.best_height = np.ctypeslib.as_array(bh).copy()
         return res
 
+    def pipeline_info(self, n_runs: int) -> dict:
+        """How msim_launch executes n_runs on the current device (msim_pipeline_info)."""
+        pl = _lib.MsimPipelineLayout()
+        check(lib.msim_pipeline_info(self._h, n_runs, ctypes.byref(pl)), "msim_pipeline_info")
+        return {f: getattr(pl, f) for f, _ in pl._fields_}
+
     # ---- device-resident form (torch tensors as HBM buffers; used by bench.py and the RCCL path)
     def workspace_bytes(self, n_runs: int) -> int:
         return int(lib.msim_workspace_bytes(self._h, n_runs))
@@ -155,6 +161,19 @@ class Simulation:
         check(lib.msim_launch(self._h, run_begin, n_runs, seed_base & 0xFFFFFFFF, ptr(d_sums), ptr(d_per_run),
                               ptr(d_best_height), ptr(d_status), ptr(d_workspace), d_workspace.numel(), sh),
               "msim_launch")
+
+
+def timing_enable(on: bool = True) -> None:
+    """Start (or stop) stage timing: HIP events on the launch stream around every msim_launch and every
+    draw kernel (K1) it issues (msim_timing_enable)."""
+    check(lib.msim_timing_enable(1 if on else 0), "msim_timing_enable")
+
+
+def timing_read() -> dict:
+    """Summed K1 / whole-launch milliseconds and launch count since the last enable/read (synchronises)."""
+    d, l, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
+    check(lib.msim_timing_read(ctypes.byref(d), ctypes.byref(l), ctypes.byref(n)), "msim_timing_read")
+    return {"draws_ms": d.value, "launch_ms": l.value, "launches": n.value}
 
 
 def sums_to_stats(sums_rows: Iterable[Sequence[int]]) -> List[MinerStats]:

@@ -219,7 +219,9 @@ def test_host_dropin_driver(msim):
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(GOLD), "..", "host")], check=True)
     # split on "\n" only: the progress line starts with "\r" like the reference's (main.cpp:219)
-    out = subprocess.run([exe, "1", "1000"], capture_output=True, text=True, check=True).stdout.rstrip("\n").split("\n")
+    # (bytes, then decode: text mode's universal newlines would turn that "\r" into "\n")
+    raw = subprocess.run([exe, "1", "1000"], capture_output=True, check=True).stdout
+    out = raw.decode().rstrip("\n").split("\n")
     assert out[0] == "Running 32768 simulations in parallel using 1 GPU(s)."
     assert out[1] == "\r100% progress.."
     assert out[2] == "After running 32768 simulations for 365d each, on average:"
