@@ -106,6 +106,25 @@ int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t
 int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t *d_out_index, uint64_t n,
                       void *stream);
 
+/* Parameter sweeps (BASELINE configs[3]: selfish share x propagation grid). The reference runs one
+ * network per build (SetupMiners, main.cpp:44-65, edited by hand per README.md:21-27); a sweep runs
+ * every point of a grid in ONE device launch, one lane per (point, run). Point p, run r gives exactly
+ * the result of msim_run(cfgs[p], run_begin, ...) for run run_begin + r (same seeds for every point).
+ * All points must have the same miner count. Sums / records are point-major:
+ *   sums[p * M + k], per_run[(p * runs_per_point + r) * M + k], best_height[p * runs_per_point + r]. */
+typedef struct msim_sweep msim_sweep;
+int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sweep **out);
+void msim_sweep_destroy(msim_sweep *sweep);
+size_t msim_sweep_workspace_bytes(const msim_sweep *sweep, uint64_t runs_per_point);
+/* Device-resident, asynchronous on `stream`; d_sums: n_points * M msim_sums; d_status as msim_launch. */
+int msim_sweep_launch(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base,
+                      void *d_sums, void *d_per_run, void *d_best_height, void *d_status, void *d_workspace,
+                      size_t workspace_bytes, void *stream);
+/* Host convenience: out_stats n_points * M (fixed-point sums converted), optional sums / records. */
+int msim_sweep_run(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base,
+                   int device, msim_stats *out_stats, msim_sums *opt_sums, msim_run_record *opt_per_run,
+                   uint32_t *opt_best_height);
+
 /* Stage timing for measurement (bench.py): while enabled, every msim_launch records HIP events on its
  * stream around the whole launch and around each draw kernel (K1, the dominant kernel of the
  * event-skipping pipeline). msim_timing_read synchronises on those events, returns the summed

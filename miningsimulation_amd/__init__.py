@@ -16,6 +16,7 @@ from .simulation import (  # noqa: F401
     MinerStats,
     Simulation,
     SimulationResult,
+    Sweep,
     c4_grid,
     exact_stats_total,
     report,

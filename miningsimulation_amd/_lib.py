@@ -37,6 +37,11 @@ EXPORTED = (
     "msim_timing_enable",
     "msim_timing_read",
     "msim_pipeline_info",
+    "msim_sweep_create",
+    "msim_sweep_destroy",
+    "msim_sweep_workspace_bytes",
+    "msim_sweep_launch",
+    "msim_sweep_run",
     "msim_strerror",
     "msim_version",
 )
@@ -124,6 +129,17 @@ def _load() -> ctypes.CDLL:
     lib.msim_timing_read.restype = ctypes.c_int
     lib.msim_pipeline_info.argtypes = [vp, u64, ctypes.POINTER(MsimPipelineLayout)]
     lib.msim_pipeline_info.restype = ctypes.c_int
+    lib.msim_sweep_create.argtypes = [ctypes.POINTER(vp), u32, ctypes.POINTER(vp)]
+    lib.msim_sweep_create.restype = ctypes.c_int
+    lib.msim_sweep_destroy.argtypes = [vp]
+    lib.msim_sweep_destroy.restype = None
+    lib.msim_sweep_workspace_bytes.argtypes = [vp, u64]
+    lib.msim_sweep_workspace_bytes.restype = sz
+    lib.msim_sweep_launch.argtypes = [vp, u64, u64, u32, vp, vp, vp, vp, vp, sz, vp]
+    lib.msim_sweep_launch.restype = ctypes.c_int
+    lib.msim_sweep_run.argtypes = [vp, u64, u64, u32, ctypes.c_int, ctypes.POINTER(MsimStats),
+                                   ctypes.POINTER(MsimSums), ctypes.POINTER(MsimRunRecord), ctypes.POINTER(u32)]
+    lib.msim_sweep_run.restype = ctypes.c_int
     lib.msim_strerror.argtypes = [ctypes.c_int]
     lib.msim_strerror.restype = ctypes.c_char_p
     lib.msim_version.argtypes = []

@@ -38,6 +38,15 @@ struct msim_config {
     std::vector<Tab> tables;  // per (device, segment length) pipeline tables, lazily uploaded
 };
 
+// A parameter sweep (BASELINE configs[3]): the points' parameter blocks, uploaded per device on first use.
+struct msim_sweep {
+    std::vector<msim::SimParams> pts;
+    uint32_t m;
+    bool self;
+    std::mutex mu;
+    std::vector<std::pair<int, void *>> dev;  // (device, SimParams[n_points])
+};
+
 namespace {
 
 uint32_t err_cap_for(uint64_t n)
@@ -65,6 +74,25 @@ WsLayout ws_layout(uint32_t m, uint64_t n)
 }
 
 constexpr uint64_t MAX_LAUNCH_RUNS = 1ull << 26;
+
+// Sweep workspace: per-workgroup partials, per-point retry sums, counters, retry list.
+struct SweepLayout {
+    size_t partials_off, retry_off, counts_off, list_off, total;
+    uint32_t wpp, err_cap;
+};
+SweepLayout sweep_layout(uint32_t m, uint32_t n_points, uint64_t rpp)
+{
+    SweepLayout l;
+    l.wpp = (uint32_t)((rpp + msim::TPB - 1) / msim::TPB);
+    l.err_cap = err_cap_for(rpp * n_points);
+    const size_t nv = 6 * (size_t)m;
+    l.partials_off = 0;
+    l.retry_off = (size_t)n_points * l.wpp * nv * 8;
+    l.counts_off = l.retry_off + (size_t)n_points * nv * 8;
+    l.list_off = l.counts_off + 256;
+    l.total = (l.list_off + (size_t)l.err_cap * 4 + 255) / 256 * 256;
+    return l;
+}
 constexpr double PIPE_MAX_RHO = 0.08;           // above this the per-lane kernel is cheaper
 constexpr double PIPE_SLICE_BUDGET = 16.0 * (1ull << 30);  // pipeline workspace per slice (bytes)
 
@@ -378,6 +406,132 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
         }
     }
 out:
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipFree(ws);
+    (void)hipFree(sums);
+    (void)hipFree(status);
+    (void)hipFree(rec);
+    (void)hipFree(bh);
+    return rc;
+}
+
+int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sweep **out)
+{
+    if (!cfgs || !out || n_points == 0) return MSIM_E_INVALID;
+    msim_sweep *w = new (std::nothrow) msim_sweep();
+    if (!w) return MSIM_E_INVALID;
+    w->m = cfgs[0] ? cfgs[0]->n : 0;
+    w->self = false;
+    for (uint32_t i = 0; i < n_points; ++i) {
+        if (!cfgs[i] || cfgs[i]->n != w->m) {  // one miner count per sweep (one kernel instantiation)
+            delete w;
+            return MSIM_E_INVALID;
+        }
+        w->pts.push_back(cfgs[i]->p);
+        w->self = w->self || cfgs[i]->p.selfish >= 0;
+    }
+    *out = w;
+    return MSIM_OK;
+}
+
+void msim_sweep_destroy(msim_sweep *sw)
+{
+    if (!sw) return;
+    for (const auto &d : sw->dev) (void)hipFree(d.second);
+    delete sw;
+}
+
+size_t msim_sweep_workspace_bytes(const msim_sweep *sw, uint64_t runs_per_point)
+{
+    if (!sw || runs_per_point == 0 || runs_per_point * sw->pts.size() > MAX_LAUNCH_RUNS) return 0;
+    return sweep_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point).total;
+}
+
+int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base,
+                      void *d_sums, void *d_per_run, void *d_best_height, void *d_status, void *d_workspace,
+                      size_t workspace_bytes, void *stream)
+{
+    if (!sw || !d_sums || !d_workspace || runs_per_point == 0) return MSIM_E_INVALID;
+    const uint32_t np = (uint32_t)sw->pts.size();
+    if (runs_per_point * np > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    const SweepLayout l = sweep_layout(sw->m, np, runs_per_point);
+    if (workspace_bytes < l.total) return MSIM_E_INVALID;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
+    void *pts = nullptr;
+    {
+        msim_sweep *w = const_cast<msim_sweep *>(sw);
+        std::lock_guard<std::mutex> g(w->mu);
+        for (const auto &d : w->dev)
+            if (d.first == dev) pts = d.second;
+        if (!pts) {
+            const size_t b = w->pts.size() * sizeof(msim::SimParams);
+            if (hipMalloc(&pts, b) != hipSuccess) return MSIM_E_HIP;
+            if (hipMemcpy(pts, w->pts.data(), b, hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipFree(pts);
+                return MSIM_E_HIP;
+            }
+            w->dev.push_back({dev, pts});
+        }
+    }
+    char *ws = (char *)d_workspace;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(ws + l.retry_off, 0, l.list_off - l.retry_off, s) != hipSuccess) return MSIM_E_HIP;
+    msim::SweepArgs a;
+    a.pts = (const msim::SimParams *)pts;
+    a.m = sw->m;
+    a.self = sw->self;
+    a.n_points = np;
+    a.rpp = (uint32_t)runs_per_point;
+    a.wpp = l.wpp;
+    a.run_begin = run_begin;
+    a.seed_base = seed_base;
+    a.partials = (uint64_t *)(ws + l.partials_off);
+    a.retry_sums = (uint64_t *)(ws + l.retry_off);
+    a.sums = (uint64_t *)d_sums;
+    a.records = (uint32_t *)d_per_run;
+    a.best_h = (uint32_t *)d_best_height;
+    a.err_count = (uint32_t *)(ws + l.counts_off);
+    a.err_list = (uint32_t *)(ws + l.list_off);
+    a.err_cap = l.err_cap;
+    a.status = (uint32_t *)d_status;
+    a.stream = s;
+    return msim::launch_sweep(a) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
+}
+
+int msim_sweep_run(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base, int device,
+                   msim_stats *out_stats, msim_sums *opt_sums, msim_run_record *opt_per_run, uint32_t *opt_best_height)
+{
+    if (!sw || !out_stats || runs_per_point == 0) return MSIM_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return MSIM_E_HIP;
+    const size_t np = sw->pts.size(), m = sw->m, nr = np * runs_per_point;
+    const size_t wsb = msim_sweep_workspace_bytes(sw, runs_per_point);
+    if (!wsb) return MSIM_E_INVALID;
+    void *ws = nullptr, *sums = nullptr, *status = nullptr, *rec = nullptr, *bh = nullptr;
+    std::vector<msim_sums> hs(np * m);
+    uint32_t st[2] = {0, 0};
+    hipStream_t s = nullptr;
+    int rc = MSIM_OK;
+    if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&sums, hs.size() * sizeof(msim_sums)) != hipSuccess ||
+        hipMalloc(&status, sizeof(st)) != hipSuccess ||
+        (opt_per_run && hipMalloc(&rec, nr * m * sizeof(msim_run_record)) != hipSuccess) ||
+        (opt_best_height && hipMalloc(&bh, nr * sizeof(uint32_t)) != hipSuccess) || hipStreamCreate(&s) != hipSuccess) {
+        rc = MSIM_E_HIP;
+    } else {
+        rc = msim_sweep_launch(sw, run_begin, runs_per_point, seed_base, sums, rec, bh, status, ws, wsb, s);
+        if (rc == MSIM_OK &&
+            (hipMemcpyAsync(hs.data(), sums, hs.size() * sizeof(msim_sums), hipMemcpyDeviceToHost, s) != hipSuccess ||
+             hipMemcpyAsync(st, status, sizeof(st), hipMemcpyDeviceToHost, s) != hipSuccess ||
+             (opt_per_run && hipMemcpyAsync(opt_per_run, rec, nr * m * sizeof(msim_run_record), hipMemcpyDeviceToHost, s) != hipSuccess) ||
+             (opt_best_height && hipMemcpyAsync(opt_best_height, bh, nr * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) ||
+             hipStreamSynchronize(s) != hipSuccess))
+            rc = MSIM_E_HIP;
+        if (rc == MSIM_OK && st[1] != 0) rc = MSIM_E_CAPACITY;
+    }
+    if (rc == MSIM_OK) {
+        if (opt_sums) memcpy(opt_sums, hs.data(), hs.size() * sizeof(msim_sums));
+        msim_sums_to_stats(hs.data(), (uint32_t)hs.size(), out_stats);
+    }
     if (s) (void)hipStreamDestroy(s);
     (void)hipFree(ws);
     (void)hipFree(sums);

@@ -57,6 +57,44 @@ hipError_t launch_runs(const LaunchArgs &a)
     }
 }
 
+// Sweep sums: point p = fixed-order sum of its workgroups' partials + its retried runs.
+__global__ void msim_sweep_finalize(const uint64_t *__restrict__ partials, uint32_t wpp, uint32_t nvals,
+                                    const uint64_t *__restrict__ retry_sums, uint64_t *__restrict__ out,
+                                    const uint32_t *__restrict__ counts, uint32_t retry_cap, uint32_t *__restrict__ status)
+{
+    const uint32_t p = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < nvals; i += blockDim.x) {
+        uint64_t s = retry_sums[(size_t)p * nvals + i];
+        for (uint32_t b = 0; b < wpp; ++b) s += partials[((size_t)p * wpp + b) * nvals + i];
+        out[(size_t)p * nvals + i] = s;
+    }
+    if (p == 0 && threadIdx.x == 0 && status) {
+        const uint32_t rc = counts[0];
+        status[0] = rc;
+        status[1] = counts[1] + (rc > retry_cap ? rc - retry_cap : 0u);
+    }
+}
+
+hipError_t launch_sweep_finalize(const SweepArgs &a)
+{
+    hipLaunchKernelGGL(msim_sweep_finalize, dim3(a.n_points), dim3(TPB), 0, a.stream, a.partials, a.wpp, 6 * a.m,
+                       a.retry_sums, a.sums, a.err_count, a.err_cap, a.status);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep(const SweepArgs &a)
+{
+    switch (a.m) {
+#define CASE(MM) \
+    case MM:     \
+        return launch_sweep_m##MM(a);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
 size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap)
 {
     const size_t nb = (n + TPB - 1) / TPB, nbr = (err_cap + TPB - 1) / TPB;

@@ -31,6 +31,35 @@ struct LaunchArgs {
 };
 
 hipError_t launch_runs(const LaunchArgs &a);
+
+// Parameter sweep (BASELINE configs[3]): every point of the sweep in ONE launch of the per-lane kernel.
+// Point p owns workgroups [p * wpp, (p + 1) * wpp); run rel of every point uses the seeds of run
+// run_begin + rel (the same runs msim_run(cfg_p, run_begin, rpp) simulates).
+struct SweepArgs {
+    const SimParams *pts;  // n_points parameter blocks in device memory
+    uint32_t m;            // miner count (same for every point)
+    bool self;             // some point has a selfish miner: use the selfish instantiation for all
+    uint32_t n_points;
+    uint32_t rpp;          // runs per point
+    uint32_t wpp;          // workgroups per point = ceil(rpp / TPB)
+    uint64_t run_begin;
+    uint32_t seed_base;
+    uint64_t *partials;    // [n_points * wpp][6M]
+    uint64_t *retry_sums;  // [n_points][6M], zeroed before the launch (retried runs add atomically)
+    uint64_t *sums;        // [n_points][6M] out
+    uint32_t *records;     // [n_points * rpp][M][2] or null
+    uint32_t *best_h;      // [n_points * rpp] or null
+    uint32_t *err_count;   // 2 u32 zeroed before the launch: [0] flagged for retry, [1] failed on retry
+    uint32_t *err_list;    // err_cap codes (point * wpp * TPB + rel)
+    uint32_t err_cap;
+    uint32_t *status;      // 2 u32 or null
+    hipStream_t stream;
+};
+hipError_t launch_sweep(const SweepArgs &a);
+#define MSIM_DECL_SWEEP(MM) hipError_t launch_sweep_m##MM(const SweepArgs &a);
+MSIM_FOR_EACH_M(MSIM_DECL_SWEEP)
+#undef MSIM_DECL_SWEEP
+hipError_t launch_sweep_finalize(const SweepArgs &a);
 #define MSIM_DECL_LAUNCH(MM) hipError_t launch_runs_m##MM(const LaunchArgs &a);
 MSIM_FOR_EACH_M(MSIM_DECL_LAUNCH)
 #undef MSIM_DECL_LAUNCH

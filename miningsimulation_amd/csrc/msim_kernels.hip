@@ -86,6 +86,85 @@ __global__ __launch_bounds__(TPB) void msim_runs_kernel(const SimParams p, const
     block_reduce_store<M>(v, partials + (size_t)blockIdx.x * 6 * M);
 }
 
+// MinerStats of one finished run (main.cpp:22-30) as the 6*M fixed-point sum terms (msim_sums layout).
+template <int M>
+__device__ __forceinline__ void stats_terms(const RunResult &r, uint64_t (&v)[6 * M])
+{
+    const double L = (double)r.best_height;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        const uint32_t f = r.found[k];
+        const double share = f == 0 ? 0.0 : (double)f / L;
+        const double rate = f == 0 ? 0.0 : (double)r.stale[k] / (double)f;
+        const uint64_t sfx = (uint64_t)(share * 4294967296.0 + 0.5);
+        const uint64_t rfx = (uint64_t)(rate * 4294967296.0 + 0.5);
+        v[6 * k + 0] = f;
+        v[6 * k + 1] = r.stale[k];
+        v[6 * k + 2] = sfx >> 32;
+        v[6 * k + 3] = sfx & 0xFFFFFFFFull;
+        v[6 * k + 4] = rfx >> 32;
+        v[6 * k + 5] = rfx & 0xFFFFFFFFull;
+    }
+}
+
+// ------------------------------------------------------------------ parameter sweep (configs[3])
+// One lane per (point, run). Workgroups never straddle points, so a wave's parameter block is
+// uniform (scalar loads from pts[point]) and its partial sums belong to one point. LIST: the retry
+// pass over flagged lanes (codes point * wpp * TPB + rel), wide capacities, atomic per-point sums.
+template <int M, bool SELF, bool DEEP, int NX, int NG, bool LIST>
+__global__ __launch_bounds__(TPB) void msim_sweep_kernel(const SimParams *__restrict__ pts, const uint64_t run_begin,
+                                                          const uint32_t rpp, const uint32_t wpp, const uint32_t seed_base,
+                                                          const uint32_t *__restrict__ list, const uint32_t *__restrict__ list_count,
+                                                          const uint32_t list_cap, uint64_t *__restrict__ partials,
+                                                          uint64_t *__restrict__ retry_sums, uint32_t *__restrict__ records,
+                                                          uint32_t *__restrict__ best_h, uint32_t *__restrict__ err_count,
+                                                          uint32_t *__restrict__ err_list, const uint32_t err_cap)
+{
+    uint32_t point, rel;
+    bool active;
+    if (LIST) {
+        const uint32_t c = *list_count, lim = c < list_cap ? c : list_cap;
+        const uint32_t idx = blockIdx.x * TPB + threadIdx.x;
+        active = idx < lim;
+        const uint32_t code = active ? list[idx] : 0u;
+        point = code / (wpp * TPB);
+        rel = code % (wpp * TPB);
+    } else {
+        point = blockIdx.x / wpp;
+        rel = (blockIdx.x % wpp) * TPB + threadIdx.x;
+        active = rel < rpp;
+    }
+    const SimParams &p = pts[point];
+    uint64_t v[6 * M];
+#pragma unroll
+    for (int i = 0; i < 6 * M; ++i) v[i] = 0;
+    if (active) {
+        const uint64_t run = run_begin + rel;
+        RunResult r;
+        Sim<M, SELF, DEEP, NX, NG> s;
+        s.run(p, rng_seed(seed_interval(seed_base, run)), rng_seed(seed_picker(seed_base, run)), r);
+        if (r.err) {
+            const uint32_t pos = atomicAdd(err_count, 1u);
+            if (!LIST && pos < err_cap) err_list[pos] = point * wpp * TPB + rel;
+        } else {
+            stats_terms<M>(r, v);
+            const size_t g = (size_t)point * rpp + rel;
+            if (records)
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    records[2 * (g * M + k) + 0] = r.found[k];
+                    records[2 * (g * M + k) + 1] = r.stale[k];
+                }
+            if (best_h) best_h[g] = r.best_height;
+            if (LIST)
+#pragma unroll
+                for (int i = 0; i < 6 * M; ++i)
+                    if (v[i]) atomicAdd((unsigned long long *)(retry_sums + (size_t)point * 6 * M + i), (unsigned long long)v[i]);
+        }
+    }
+    if (!LIST) block_reduce_store<M>(v, partials + (size_t)blockIdx.x * 6 * M);
+}
+
 // ------------------------------------------------------------------ event-skipping pipeline (K2, K3)
 // K2: one lane per listed non-fast block (msim_pipeline.h episode_entry).
 template <int M>
@@ -258,11 +337,36 @@ static hipError_t launch_m(const LaunchArgs &a)
                            a.status, a.stream);
 }
 
+template <int M>
+static hipError_t launch_sweep_impl(const SweepArgs &a)
+{
+    const uint32_t nb = a.n_points * a.wpp, nbr = (a.err_cap + TPB - 1) / TPB;
+    if (a.self) {
+        hipLaunchKernelGGL((msim_sweep_kernel<M, true, true, NX_FAST, NG_FAST, false>), dim3(nb), dim3(TPB), 0, a.stream,
+                           a.pts, a.run_begin, a.rpp, a.wpp, a.seed_base, nullptr, nullptr, 0u, a.partials, a.retry_sums,
+                           a.records, a.best_h, a.err_count, a.err_list, a.err_cap);
+        hipLaunchKernelGGL((msim_sweep_kernel<M, true, true, NX_WIDE, NG_WIDE, true>), dim3(nbr), dim3(TPB), 0, a.stream,
+                           a.pts, a.run_begin, a.rpp, a.wpp, a.seed_base, a.err_list, a.err_count, a.err_cap, a.partials,
+                           a.retry_sums, a.records, a.best_h, a.err_count + 1, nullptr, 0u);
+    } else {
+        hipLaunchKernelGGL((msim_sweep_kernel<M, false, false, NX_FAST, NG_FAST, false>), dim3(nb), dim3(TPB), 0, a.stream,
+                           a.pts, a.run_begin, a.rpp, a.wpp, a.seed_base, nullptr, nullptr, 0u, a.partials, a.retry_sums,
+                           a.records, a.best_h, a.err_count, a.err_list, a.err_cap);
+        hipLaunchKernelGGL((msim_sweep_kernel<M, false, true, NX_WIDE, NG_WIDE, true>), dim3(nbr), dim3(TPB), 0, a.stream,
+                           a.pts, a.run_begin, a.rpp, a.wpp, a.seed_base, a.err_list, a.err_count, a.err_cap, a.partials,
+                           a.retry_sums, a.records, a.best_h, a.err_count + 1, nullptr, 0u);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_sweep_finalize(a);
+}
+
 #if defined(MSIM_M)
 // One translation unit per miner count (built in parallel): explicit entry point for M = MSIM_M.
 #define MSIM_CAT2(a, b) a##b
 #define MSIM_CAT(a, b) MSIM_CAT2(a, b)
 hipError_t MSIM_CAT(launch_runs_m, MSIM_M)(const LaunchArgs &a) { return launch_m<MSIM_M>(a); }
+hipError_t MSIM_CAT(launch_sweep_m, MSIM_M)(const SweepArgs &a) { return launch_sweep_impl<MSIM_M>(a); }
 #endif
 
 }  // namespace msim

@@ -163,6 +163,68 @@ class Simulation:
               "msim_launch")
 
 
+class Sweep:
+    """A grid of networks run in ONE device launch (BASELINE configs[3]; msim_sweep_* in include/msim.h).
+
+    The reference covers a grid by editing SetupMiners (main.cpp:44-65) and rebuilding per point
+    (README.md:21-27). Point p, run r of a sweep is bit-identical to Simulation(points[p]).run for run
+    run_begin + r: every point sees the same seeds."""
+
+    def __init__(self, points: Sequence[Sequence[Miner]], duration_ms: int = SIM_DURATION_MS):
+        self.sims = [Simulation(p, duration_ms) for p in points]
+        self.m = len(self.sims[0].miners)
+        handles = (ctypes.c_void_p * len(self.sims))(*[s.handle.value for s in self.sims])
+        h = ctypes.c_void_p()
+        check(lib.msim_sweep_create(handles, len(self.sims), ctypes.byref(h)), "msim_sweep_create")
+        self._h = h
+
+    def __len__(self) -> int:
+        return len(self.sims)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.msim_sweep_destroy(h)
+            self._h = None
+
+    def run(self, runs_per_point: int, run_begin: int = 0, seed_base: int = DEFAULT_SEED_BASE, device: int = 0,
+            per_run: bool = False) -> List[SimulationResult]:
+        n, m = len(self.sims), self.m
+        stats = (MsimStats * (n * m))()
+        sums = (MsimSums * (n * m))()
+        rec = (MsimRunRecord * (n * runs_per_point * m))() if per_run else None
+        bh = (ctypes.c_uint32 * (n * runs_per_point))() if per_run else None
+        check(lib.msim_sweep_run(self._h, run_begin, runs_per_point, seed_base & 0xFFFFFFFF, device, stats, sums, rec, bh),
+              "msim_sweep_run")
+        out = []
+        for p in range(n):
+            res = SimulationResult(
+                stats_total=[MinerStats(s.blocks_found, s.blocks_share, s.stale_rate) for s in stats[p * m:(p + 1) * m]],
+                sums=list(sums[p * m:(p + 1) * m]),
+                n_runs=runs_per_point,
+            )
+            if per_run:
+                a = np.ctypeslib.as_array(ctypes.cast(rec, ctypes.POINTER(ctypes.c_uint32)),
+                                          shape=(n, runs_per_point, m, 2))
+                res.found = a[p, :, :, 0].copy()
+                res.stale = a[p, :, :, 1].copy()
+                res.best_height = np.ctypeslib.as_array(bh).reshape(n, runs_per_point)[p].copy()
+            out.append(res)
+        return out
+
+    def workspace_bytes(self, runs_per_point: int) -> int:
+        return int(lib.msim_sweep_workspace_bytes(self._h, runs_per_point))
+
+    def launch(self, runs_per_point: int, run_begin: int, seed_base: int, d_sums, d_workspace, d_status,
+               d_per_run=None, d_best_height=None, stream=None) -> None:
+        """Asynchronous launch on the current device; d_sums: int64 [n_points, M, 6]."""
+        ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+        sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        check(lib.msim_sweep_launch(self._h, run_begin, runs_per_point, seed_base & 0xFFFFFFFF, ptr(d_sums),
+                                    ptr(d_per_run), ptr(d_best_height), ptr(d_status), ptr(d_workspace),
+                                    d_workspace.numel(), sh), "msim_sweep_launch")
+
+
 def timing_enable(on: bool = True) -> None:
     """Start (or stop) stage timing: HIP events on the launch stream around every msim_launch and every
     draw kernel (K1) it issues (msim_timing_enable)."""

@@ -158,6 +158,41 @@ def test_gpu_c4_grid_sample(msim, oracle):
         assert np.array_equal(res.stale.astype(np.int64), st), (p, q)
 
 
+def test_gpu_sweep_vs_oracle(msim, oracle):
+    """One sweep launch over 12 grid points (BASELINE configs[3]) against the oracle run by run: every
+    point sees the seeds of runs [run_begin, run_begin + n), like msim_run(cfg_p, run_begin, n)."""
+    rng = random.Random(11)
+    pts = rng.sample(msim.c4_grid(), 12)
+    n, begin = 48, 5000
+    out = msim.Sweep(pts).run(n, begin, 1000, 0, per_run=True)
+    for miners, res in zip(pts, out):
+        p = [m.perc for m in miners]
+        q = [m.propagation_ms for m in miners]
+        s = [m.is_selfish for m in miners]
+        f, st, _, _ = oracle.run_batch(p, q, s, D, n, begin, 1000, threads=16)
+        assert np.array_equal(res.found.astype(np.int64), f), (p, q)
+        assert np.array_equal(res.stale.astype(np.int64), st), (p, q)
+        assert np.array_equal(res.found.sum(axis=1), res.best_height)
+
+
+def test_gpu_sweep_equals_single_runs(msim):
+    """Mixed sweep (honest networks through the selfish instantiation, runs per point not a multiple of
+    the workgroup) == msim_run per point: same fixed-point sums, same per-run counters. For the honest
+    points msim_run takes the event-skipping pipeline, so this also cross-checks two device paths."""
+    pts = [msim.setup_miners(1000, selfish_perc=25), msim.setup_miners(100), msim.setup_miners(30000, selfish_perc=45),
+           msim.setup_miners(10000)]
+    n = 1000
+    out = msim.Sweep(pts).run(n, 123, 1000, 0, per_run=True)
+    for miners, res in zip(pts, out):
+        one = msim.Simulation(miners).run(n, 123, 1000, 0, per_run=True)
+        assert np.array_equal(res.found, one.found)
+        assert np.array_equal(res.stale, one.stale)
+        assert np.array_equal(res.best_height, one.best_height)
+        no_rec = msim.Simulation(miners).run(n, 123, 1000, 0)
+        for a, b in zip(res.sums, no_rec.sums):
+            assert bytes(a) == bytes(b)
+
+
 def test_gpu_retry_path_huge_delays(msim, oracle):
     """Delays of minutes overflow the fast kernel's in-flight capacity; the retry kernel must take those
     runs and still match the oracle."""
