@@ -47,8 +47,9 @@ def cpu_baseline(preset: str, sample_runs: int, threads: int, target_s: float = 
         return json.loads(out.stdout.splitlines()[0])
 
     if not sample_runs:  # calibrate on a small sample, then size the real sample to ~target_s seconds
-        probe = timed(threads * 16)
-        sample_runs = max(threads * 16, int(probe["run_years_per_s"] * target_s) // threads * threads)
+        per = 1 if preset == "c5" else 16  # c5: ~1 run-year/s per core (explicit chains, 1026 miners)
+        probe = timed(threads * per)
+        sample_runs = max(threads * per, int(probe["run_years_per_s"] * target_s) // threads * threads)
     rec = timed(sample_runs)
     return {
         "value": round(rec["run_years_per_s"], 2),
@@ -65,8 +66,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "default"])
-    ap.add_argument("--runs", type=int, default=32768, help="runs per GPU per step")
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5", "default"])
+    ap.add_argument("--runs", type=int, default=0, help="runs per GPU per step (0: 32768; c5: 65536)")
     ap.add_argument("--seed-base", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
@@ -84,11 +85,12 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from miningsimulation_amd import PRESETS, Simulation, timing_enable, timing_read
+    from miningsimulation_amd.simulation import PRESET_WEIGHTS
 
     miners = PRESETS[args.config]()
     m = len(miners)
-    sim = Simulation(miners)
-    n = args.runs
+    sim = Simulation(miners, total_weight=PRESET_WEIGHTS.get(args.config, 100))
+    n = args.runs or (65536 if args.config == "c5" else 32768)
     dev = torch.device("cuda", local)
     ws = torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev)
     sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
@@ -158,8 +160,10 @@ def main() -> None:
             "dtype": "int64+fp64",
             "data": "synthetic (seeded runs; run r uses rd()-equivalents (base+2r, base+2r+1))",
             "config": {
-                "workload": f"{args.config}: BASELINE configs[1]" if args.config == "c2" else args.config,
-                "network": [[mm.id, mm.perc, mm.propagation_ms, int(mm.is_selfish)] for mm in miners],
+                "workload": {"c2": "c2: BASELINE configs[1]", "c3": "c3: BASELINE configs[2]",
+                             "c5": "c5: BASELINE configs[4] (SURVEY Appendix C weights, W=102400)"}.get(args.config, args.config),
+                "network": ([[mm.id, mm.perc, mm.propagation_ms, int(mm.is_selfish)] for mm in miners] if m <= 16 else
+                            f"{m} miners: weights 30720, 29696, 1024 x 41 (W=102400), all honest, prop 1000 ms"),
                 "runs_per_gpu_per_step": n,
                 "duration": "months{12} = 31556952000 ms",
                 "parallelism": f"runs sharded over {world} GPU(s), RCCL all-reduce of per-miner integer sums",
@@ -172,8 +176,9 @@ def main() -> None:
                 "unit": "T lane-op/s",
                 "frac": round(achieved / VALU_PEAK_LANE_OPS, 5),
                 "traffic": None,
-                "kernel": "msim_launch = K1 msim_draws_kernel + K2 episodes + K3 combine + finalize "
-                          "(HIP events on the launch stream; conservative: the whole launch, not K1 alone)",
+                "kernel": ("msim_launch = W1 msim_wide_draws_kernel + W2 episodes + W3 combine" if sim.wide else
+                           "msim_launch = K1 msim_draws_kernel + K2 episodes + K3 combine + finalize") +
+                          " (HIP events on the launch stream; conservative: the whole launch, not the draw kernel alone)",
                 "kernel_ms": round(kern_ms, 4),
                 "k1_ms": round(k1_ms, 4),
                 "k1_share": round(k1_ms / kern_ms, 4) if kern_ms > 0 else None,

@@ -29,14 +29,15 @@ extern "C" {
 
 #define MSIM_OK 0
 #define MSIM_E_INVALID (-1)  /* bad argument (null pointer, n == 0, negative duration/propagation) */
-#define MSIM_E_WEIGHTS (-2)  /* percentages above 100 in total (reference: u64 wrap / assert) */
+#define MSIM_E_WEIGHTS (-2)  /* weights do not add up to 100 (or total_weight): the reference asserts */
 #define MSIM_E_SELFISH (-3)  /* more than one selfish miner (device path supports at most one) */
-#define MSIM_E_MINERS (-4)   /* more than MSIM_MAX_MINERS miners, or duplicate miner ids */
+#define MSIM_E_MINERS (-4)   /* too many miners (see MSIM_MAX_*_MINERS), or duplicate miner ids */
 #define MSIM_E_HIP (-5)      /* HIP runtime error (no device, launch failure, out of memory) */
 #define MSIM_E_CAPACITY (-6) /* a run exceeded the compact state's capacity even on the retry kernel */
 #define MSIM_E_PICK (-7)     /* PickFinder fell through (simulation.h:220 assert): percentages < 100 */
 
-#define MSIM_MAX_MINERS 15
+#define MSIM_MAX_MINERS 15        /* networks with a selfish miner (compact per-lane state) */
+#define MSIM_MAX_WIDE_MINERS 4096 /* honest networks (large-network pipeline, BASELINE configs[4]) */
 
 typedef struct msim_miner {
     uint32_t id;            /* Miner::id (simulation.h:43) */
@@ -71,6 +72,17 @@ typedef struct msim_run_record {
 } msim_run_record;
 
 int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms, msim_config **out);
+/* Weight generalisation (not expressible in the reference, whose perc are integer
+ * percentages, simulation.h:45, main.cpp:43): `perc` holds integer weights that must add up to
+ * total_weight W < 2^31, and PickFinder uses UINT64_MAX / W in place of PERC_MULTIPLIER
+ * (simulation.h:18, 217). W = 100 is exactly msim_config_create. Honest networks of more than
+ * MSIM_MAX_MINERS miners (up to MSIM_MAX_WIDE_MINERS), or with W != 100, run on the large-network
+ * pipeline; a selfish miner is supported only with W = 100 and n <= MSIM_MAX_MINERS. */
+int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
+                                msim_config **out);
+/* 1 when the config runs on the large-network pipeline (set MSIM_FORCE_WIDE=1 in the environment before
+ * msim_config_create to route small honest networks there too, e.g. for cross-path parity checks). */
+int msim_config_is_wide(const msim_config *cfg);
 void msim_config_destroy(msim_config *cfg);
 uint32_t msim_config_miner_count(const msim_config *cfg);
 

@@ -25,6 +25,8 @@ MSIM_MAX_MINERS = 15
 # Every symbol include/msim.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "msim_config_create",
+    "msim_config_create_weighted",
+    "msim_config_is_wide",
     "msim_config_destroy",
     "msim_config_miner_count",
     "msim_run",
@@ -103,6 +105,10 @@ def _load() -> ctypes.CDLL:
     vp, u32, u64, i64, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64, ctypes.c_size_t
     lib.msim_config_create.argtypes = [ctypes.POINTER(MsimMiner), u32, i64, ctypes.POINTER(vp)]
     lib.msim_config_create.restype = ctypes.c_int
+    lib.msim_config_create_weighted.argtypes = [ctypes.POINTER(MsimMiner), u32, i64, u64, ctypes.POINTER(vp)]
+    lib.msim_config_create_weighted.restype = ctypes.c_int
+    lib.msim_config_is_wide.argtypes = [vp]
+    lib.msim_config_is_wide.restype = ctypes.c_int
     lib.msim_config_destroy.argtypes = [vp]
     lib.msim_config_destroy.restype = None
     lib.msim_config_miner_count.argtypes = [vp]

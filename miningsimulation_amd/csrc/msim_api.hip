@@ -9,12 +9,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
 #include "../../include/msim.h"
 #include "msim_jump.h"
 #include "msim_kernels.h"
+#include "msim_wide_launch.h"
 
 namespace {
 constexpr int MAX_DEVICES = 64;
@@ -36,6 +38,13 @@ struct msim_config {
         void *ptr;
     };
     std::vector<Tab> tables;  // per (device, segment length) pipeline tables, lazily uploaded
+    // Large honest networks (msim_wide.h): any miner count up to WIDE_MAX_M, integer weights summing to W.
+    bool wide = false;
+    uint64_t total_weight = 100;
+    std::vector<uint32_t> wids;
+    std::vector<uint64_t> wperc;
+    std::vector<int64_t> wprop;
+    std::vector<std::pair<int, void *>> wtables;  // per device: pick, fast-threshold, prop, log, jump tables
 };
 
 // A parameter sweep (BASELINE configs[3]): the points' parameter blocks, uploaded per device on first use.
@@ -186,57 +195,216 @@ int global_log_table(const msim::LogEntry **out)
     return MSIM_OK;
 }
 
+constexpr double WIDE_SLICE_BUDGET = 16.0 * (1ull << 30);
+
+msim::WideLayout wide_layout(const msim_config *c, uint64_t n_runs)
+{
+    return msim::wide_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, WIDE_SLICE_BUDGET);
+}
+
+// Device tables of a wide config (msim_wide_launch.h WideArgs) on the current device, uploaded once.
+int wide_tables(msim_config *c, msim::WideArgs *a)
+{
+    using namespace msim;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
+    const uint32_t m = c->n;
+    const WideGeom g = wide_geom(c->p.duration_ms);
+    const size_t o_cumw = 0, o_bkt = o_cumw + 4 * (size_t)m, o_fthr = o_bkt + 4 * (size_t)WB_N;
+    const size_t o_prop = (o_fthr + 4 * (size_t)m + 7) / 8 * 8, o_log = o_prop + 8 * (size_t)m;
+    const size_t o_jm = (o_log + LOG_TAB * sizeof(LogEntry) + 255) / 256 * 256, o_jt = o_jm + 64 * 2048,
+                 o_js = o_jt + 64 * 2048, total = o_js + 2048;
+    std::lock_guard<std::mutex> lk(c->mu);
+    void *d = nullptr;
+    for (const auto &t : c->wtables)
+        if (t.first == dev) d = t.second;
+    if (!d) {
+        std::vector<char> h(total, 0);
+        build_wide_pick(c->wperc.data(), m, (uint32_t)c->total_weight, (uint32_t *)(h.data() + o_cumw),
+                        (uint32_t *)(h.data() + o_bkt));
+        for (uint32_t k = 0; k < m; ++k) {
+            ((uint32_t *)(h.data() + o_fthr))[k] =
+                c->wprop[k] < (int64_t)FTHR_NEVER ? (uint32_t)c->wprop[k] : FTHR_NEVER;
+            ((int64_t *)(h.data() + o_prop))[k] = c->wprop[k];
+        }
+        build_log_table((LogEntry *)(h.data() + o_log));
+        // jmain[l] = T^(l*S0); jtail[l] = T^(B0 + l*ST); jstep = T^(63*ST - 1)
+        auto store = [](const Mat128 &mm, uint32_t *w) {
+            for (int col = 0; col < 128; ++col) {
+                w[4 * col + 0] = (uint32_t)mm.lo[col];
+                w[4 * col + 1] = (uint32_t)(mm.lo[col] >> 32);
+                w[4 * col + 2] = (uint32_t)mm.hi[col];
+                w[4 * col + 3] = (uint32_t)(mm.hi[col] >> 32);
+            }
+        };
+        build_jump_table(64, g.S0, (uint32_t *)(h.data() + o_jm));
+        {
+            Mat128 step, cur, tmp;
+            mat_pow(g.B0, cur);
+            mat_pow(g.ST, step);
+            for (uint32_t l = 0; l < 64; ++l) {
+                store(cur, (uint32_t *)(h.data() + o_jt) + (size_t)l * 512);
+                mat_mul(step, cur, tmp);
+                cur = tmp;
+            }
+            mat_pow(63ull * g.ST - 1, tmp);
+            store(tmp, (uint32_t *)(h.data() + o_js));
+        }
+        if (hipMalloc(&d, total) != hipSuccess) return MSIM_E_HIP;
+        if (hipMemcpy(d, h.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return MSIM_E_HIP;
+        }
+        c->wtables.push_back({dev, d});
+    }
+    const char *b = (const char *)d;
+    a->cumw = (const uint32_t *)(b + o_cumw);
+    a->bucket = (const uint32_t *)(b + o_bkt);
+    a->fthr = (const uint32_t *)(b + o_fthr);
+    a->prop = (const int64_t *)(b + o_prop);
+    a->logt = (const LogEntry *)(b + o_log);
+    a->jmain = (const uint32_t *)(b + o_jm);
+    a->jtail = (const uint32_t *)(b + o_jt);
+    a->jstep = (const uint32_t *)(b + o_js);
+    a->m = m;
+    a->W = (uint32_t)c->total_weight;
+    a->mult = 0xFFFFFFFFFFFFFFFFull / c->total_weight;
+    a->D = c->p.duration_ms;
+    a->S0 = g.S0;
+    a->ST = g.ST;
+    a->nch = g.nch;
+    a->B0 = g.B0;
+    return MSIM_OK;
+}
+
+// Validate a miner list with integer weights summing to total_weight and build the config.
+int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
+                       msim_config **out)
+{
+    if (!miners || !out || n == 0 || duration_ms < 0 || total_weight == 0) return MSIM_E_INVALID;
+    if (n > msim::WIDE_MAX_M) return MSIM_E_MINERS;
+    if (total_weight >= (1ull << 31)) return MSIM_E_WEIGHTS;
+    {
+        std::vector<uint32_t> ids(n);
+        for (uint32_t k = 0; k < n; ++k) ids[k] = miners[k].id;
+        std::sort(ids.begin(), ids.end());
+        for (uint32_t k = 1; k < n; ++k)
+            if (ids[k] == ids[k - 1]) return MSIM_E_MINERS;
+    }
+    uint64_t total = 0;
+    uint32_t nself = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (miners[k].propagation_ms < 0) return MSIM_E_INVALID;
+        if (miners[k].perc > total_weight) return MSIM_E_WEIGHTS;
+        total += miners[k].perc;
+        nself += miners[k].is_selfish ? 1u : 0u;
+    }
+    // "Must add up to 1" (main.cpp:43); anything else makes PickFinder assert (simulation.h:220).
+    if (total != total_weight) return MSIM_E_WEIGHTS;
+    if (nself > 1) return MSIM_E_SELFISH;
+    const bool narrow = n <= MSIM_MAX_MINERS && total_weight == 100;
+    const bool force_wide = getenv("MSIM_FORCE_WIDE") != nullptr && nself == 0;
+    if (!narrow && nself) return MSIM_E_SELFISH;  // the large-network path is honest-only
+    msim_config *c = new (std::nothrow) msim_config();
+    if (!c) return MSIM_E_INVALID;
+    c->n = n;
+    c->total_weight = total_weight;
+    c->p.duration_ms = duration_ms;
+    c->p.m = (int32_t)n;
+    c->p.selfish = -1;
+    double rho = 0.0;
+    for (uint32_t k = 0; k < n; ++k)
+        rho += (double)miners[k].perc / (double)total_weight *
+               (miners[k].is_selfish ? 1.0 : 1.0 - exp(-((double)miners[k].propagation_ms + 1.0) / 599999.5));
+    c->rho = rho;
+    if (narrow && !force_wide) {
+        for (uint32_t k = 0; k < n; ++k) {
+            c->ids[k] = miners[k].id;
+            c->perc[k] = miners[k].perc;
+            c->prop[k] = miners[k].propagation_ms;
+            c->self[k] = miners[k].is_selfish ? 1 : 0;
+        }
+        const int rc = msim::make_params(c->perc, c->prop, c->self, (int)n, duration_ms, &c->p);
+        if (rc) {
+            delete c;
+            return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
+        }
+        c->pipe_ok = c->p.selfish < 0 && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
+    } else {
+        c->wide = true;
+        c->pipe_ok = false;
+        c->wids.resize(n);
+        c->wperc.resize(n);
+        c->wprop.resize(n);
+        for (uint32_t k = 0; k < n; ++k) {
+            c->wids[k] = miners[k].id;
+            c->wperc[k] = miners[k].perc;
+            c->wprop[k] = miners[k].propagation_ms;
+        }
+        const msim::WideLayout L = wide_layout(c, 1);
+        if (msim::wide_w3_lds(n, L.rcap, L.g.nch) > 160 * 1024) {  // fork rate too high for the wide combine
+            delete c;
+            return MSIM_E_CAPACITY;
+        }
+    }
+    *out = c;
+    return MSIM_OK;
+}
+
+int launch_wide_cfg(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, void *d_sums,
+                    void *d_per_run, void *d_best_height, void *d_status, void *d_workspace, size_t workspace_bytes,
+                    void *stream, std::vector<hipEvent_t> *w1_events)
+{
+    const msim::WideLayout L = wide_layout(cfg, n_runs);
+    const size_t head = 256;
+    if (workspace_bytes < head + L.total) return MSIM_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    char *ws = (char *)d_workspace;
+    uint32_t *counts = (uint32_t *)ws;
+    if (hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(d_sums, 0, 6 * sizeof(uint64_t) * cfg->n, s) != hipSuccess)
+        return MSIM_E_HIP;
+    msim::WideArgs a;
+    int rc = wide_tables(const_cast<msim_config *>(cfg), &a);
+    if (rc) return rc;
+    a.seed_base = seed_base;
+    a.rcap = L.rcap;
+    msim::WideOut o;
+    o.sums = (uint64_t *)d_sums;
+    o.records = (uint32_t *)d_per_run;
+    o.best_h = (uint32_t *)d_best_height;
+    o.fail = counts + 1;
+    o.run_begin = run_begin;
+    o.n_total = n_runs;
+    o.rel_begin = 0;
+    if (msim::launch_wide(a, L, ws + head, o, s, w1_events) != hipSuccess) return MSIM_E_HIP;
+    if (d_status && hipMemcpyAsync(d_status, counts, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return MSIM_E_HIP;
+    return MSIM_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms, msim_config **out)
 {
-    if (!miners || !out || n == 0 || duration_ms < 0) return MSIM_E_INVALID;
-    if (n > MSIM_MAX_MINERS) return MSIM_E_MINERS;
-    uint64_t perc[MSIM_MAX_MINERS];
-    int64_t prop[MSIM_MAX_MINERS];
-    uint8_t self[MSIM_MAX_MINERS];
-    uint64_t total = 0;
-    for (uint32_t k = 0; k < n; ++k) {
-        for (uint32_t j = 0; j < k; ++j)
-            if (miners[j].id == miners[k].id) return MSIM_E_MINERS;
-        perc[k] = miners[k].perc;
-        prop[k] = miners[k].propagation_ms;
-        self[k] = miners[k].is_selfish ? 1 : 0;
-        if (prop[k] < 0) return MSIM_E_INVALID;
-        if (perc[k] > 100) return MSIM_E_WEIGHTS;
-        total += perc[k];
-    }
-    // "Must add up to 1" (main.cpp:43); anything else makes PickFinder assert (simulation.h:220).
-    if (total != 100) return MSIM_E_WEIGHTS;
-    msim_config *c = new (std::nothrow) msim_config();
-    if (!c) return MSIM_E_INVALID;
-    const int rc = msim::make_params(perc, prop, self, (int)n, duration_ms, &c->p);
-    if (rc) {
-        delete c;
-        return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
-    }
-    c->n = n;
-    double rho = 0.0;
-    for (uint32_t k = 0; k < n; ++k) {
-        c->ids[k] = miners[k].id;
-        c->perc[k] = perc[k];
-        c->prop[k] = prop[k];
-        c->self[k] = self[k];
-        // P(next interval <= prop): the block is not fast (msim_pipeline.h)
-        rho += (double)perc[k] / 100.0 * (self[k] ? 1.0 : 1.0 - exp(-((double)prop[k] + 1.0) / 599999.5));
-    }
-    c->rho = rho;
-    c->pipe_ok = c->p.selfish < 0 && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
-    *out = c;
-    return MSIM_OK;
+    return config_create_impl(miners, n, duration_ms, 100u, out);
 }
+
+int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
+                                msim_config **out)
+{
+    return config_create_impl(miners, n, duration_ms, total_weight, out);
+}
+
+int msim_config_is_wide(const msim_config *cfg) { return cfg && cfg->wide ? 1 : 0; }
 
 void msim_config_destroy(msim_config *cfg)
 {
     if (!cfg) return;
     for (const auto &t : cfg->tables) (void)hipFree(t.ptr);
+    for (const auto &t : cfg->wtables) (void)hipFree(t.second);
     delete cfg;
 }
 
@@ -245,6 +413,7 @@ uint32_t msim_config_miner_count(const msim_config *cfg) { return cfg ? cfg->n :
 size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
 {
     if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
+    if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
     size_t t = ws_layout(cfg->n, n_runs).total;
     if (cfg->pipe_ok) t += pipe_layout(cfg, n_runs).total;
     return t;
@@ -255,6 +424,27 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
                 void *stream)
 {
     if (!cfg || !d_sums || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    if (cfg->wide) {
+        Timing &tm = timing();
+        std::unique_lock<std::mutex> lk(tm.mu);
+        hipEvent_t lb = nullptr, le = nullptr;
+        std::vector<hipEvent_t> *w1 = nullptr;
+        if (tm.on) {
+            w1 = &tm.k1;
+            if (hipEventCreate(&lb) == hipSuccess && hipEventCreate(&le) == hipSuccess) {
+                tm.launch.push_back(lb);
+                tm.launch.push_back(le);
+                (void)hipEventRecord(lb, (hipStream_t)stream);
+            }
+            tm.launches++;
+        } else {
+            lk.unlock();
+        }
+        const int rc = launch_wide_cfg(cfg, run_begin, n_runs, seed_base, d_sums, d_per_run, d_best_height, d_status,
+                                       d_workspace, workspace_bytes, stream, w1);
+        if (le) (void)hipEventRecord(le, (hipStream_t)stream);
+        return rc;
+    }
     const WsLayout l = ws_layout(cfg->n, n_runs);
     msim::PipeLayout pl;
     if (cfg->pipe_ok) pl = pipe_layout(cfg, n_runs);
@@ -324,6 +514,13 @@ int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t
 int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t *d_out_index, uint64_t n, void *stream)
 {
     if (!cfg || !d_uniform || !d_out_index) return MSIM_E_INVALID;
+    if (cfg->wide) {
+        msim::WideArgs a;
+        const int rc = wide_tables(const_cast<msim_config *>(cfg), &a);
+        if (rc) return rc;
+        return msim::launch_wide_picks(a, d_uniform, d_out_index, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK
+                                                                                                         : MSIM_E_HIP;
+    }
     msim::PipeTables t;
     const msim::PipeLayout pl = pipe_layout(cfg, 1);
     const int rc = device_tables(const_cast<msim_config *>(cfg), pl.seg, pl.nseg, &t);
@@ -423,7 +620,7 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
     w->m = cfgs[0] ? cfgs[0]->n : 0;
     w->self = false;
     for (uint32_t i = 0; i < n_points; ++i) {
-        if (!cfgs[i] || cfgs[i]->n != w->m) {  // one miner count per sweep (one kernel instantiation)
+        if (!cfgs[i] || cfgs[i]->n != w->m || cfgs[i]->wide) {  // one miner count per sweep; narrow networks
             delete w;
             return MSIM_E_INVALID;
         }
@@ -582,6 +779,16 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     if (!cfg || !out || n_runs == 0) return MSIM_E_INVALID;
     memset(out, 0, sizeof(*out));
     out->rho = cfg->rho;
+    if (cfg->wide) {
+        const msim::WideLayout L = wide_layout(cfg, n_runs);
+        out->uses_pipeline = 2;
+        out->slice_runs = L.nr;
+        out->segment_blocks = L.g.S0;
+        out->segments = 64;
+        out->blocks_per_run = L.g.B0 + 64ull * L.g.ST * L.g.nch;
+        out->workspace_bytes = L.total;
+        return MSIM_OK;
+    }
     if (!cfg->pipe_ok) return MSIM_OK;
     const msim::PipeLayout pl = pipe_layout(cfg, n_runs);
     out->uses_pipeline = 1;
@@ -598,9 +805,9 @@ const char *msim_strerror(int code)
     switch (code) {
     case MSIM_OK: return "ok";
     case MSIM_E_INVALID: return "invalid argument";
-    case MSIM_E_WEIGHTS: return "miner percentages must be integers in [0,100] adding up to 100";
+    case MSIM_E_WEIGHTS: return "miner weights must be integers adding up to the total weight (100 for percentages)";
     case MSIM_E_SELFISH: return "at most one selfish miner is supported on the device path";
-    case MSIM_E_MINERS: return "too many miners (max 15) or duplicate miner ids";
+    case MSIM_E_MINERS: return "too many miners (max 4096; networks with a selfish miner: 15) or duplicate miner ids";
     case MSIM_E_HIP: return "HIP runtime error";
     case MSIM_E_CAPACITY: return "a run exceeded the compact state capacity";
     case MSIM_E_PICK: return "PickFinder fell through its table";

@@ -1,0 +1,473 @@
+// msim_wide.hip — gfx950 kernels of the large-network pipeline (msim_wide.h): W1 draws + LDS histogram
+// (one wave per run), W2 episodes (one lane per candidate), W3 combine + MinerStats sums (one wave per run).
+//
+// Roofline: W1 is VALU-issue bound like the narrow K1 (two xoroshiro128++ steps, the FP64 interval and a
+// bucketed weighted pick per block, one LDS atomic); W2/W3 are short latency-bound passes over ~rho of
+// the blocks and M counters per run. HBM traffic is ~4 KiB of histogram per run plus ~rho * blocks
+// candidate records: far below the HBM roofline.
+#include <hip/hip_runtime.h>
+
+#include "msim_jump.h"
+#include "msim_wide_launch.h"
+
+namespace msim {
+
+__device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
+
+namespace {
+
+// Both RNG states advanced by one 128x128 GF(2) matrix (msim_jump.h layout). `cols` may differ per lane.
+__device__ __forceinline__ void jump_both(const uint4 *__restrict__ cols, Rng &a, Rng &b)
+{
+    const uint32_t sa[4] = {(uint32_t)a.s0, (uint32_t)(a.s0 >> 32), (uint32_t)a.s1, (uint32_t)(a.s1 >> 32)};
+    const uint32_t sb[4] = {(uint32_t)b.s0, (uint32_t)(b.s0 >> 32), (uint32_t)b.s1, (uint32_t)(b.s1 >> 32)};
+    uint32_t oa0 = 0, oa1 = 0, oa2 = 0, oa3 = 0, ob0 = 0, ob1 = 0, ob2 = 0, ob3 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) {
+            const uint4 c = cols[w * 32 + i];
+            const uint32_t ma = 0u - ((sa[w] >> i) & 1u), mb = 0u - ((sb[w] >> i) & 1u);
+            oa0 ^= c.x & ma;
+            oa1 ^= c.y & ma;
+            oa2 ^= c.z & ma;
+            oa3 ^= c.w & ma;
+            ob0 ^= c.x & mb;
+            ob1 ^= c.y & mb;
+            ob2 ^= c.z & mb;
+            ob3 ^= c.w & mb;
+        }
+    }
+    a.s0 = (uint64_t)oa0 | ((uint64_t)oa1 << 32);
+    a.s1 = (uint64_t)oa2 | ((uint64_t)oa3 << 32);
+    b.s0 = (uint64_t)ob0 | ((uint64_t)ob1 << 32);
+    b.s1 = (uint64_t)ob2 | ((uint64_t)ob3 << 32);
+}
+
+__device__ __forceinline__ uint64_t wave_excl_scan(uint64_t x, uint32_t lane)
+{
+    uint64_t v = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up((unsigned long long)v, o, 64);
+        if ((int)lane >= o) v += y;
+    }
+    return v - x;
+}
+
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
+
+struct W1Lds {
+    const uint32_t *cumw, *fthr, *bucket;
+    uint32_t *hist;  // this wave's run
+    uint32_t *cc;    // this wave's candidate counter
+};
+
+// Lane segment of nblk blocks starting at block b0 (RNG states positioned at draw b0).
+__device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogEntry *__restrict__ lt, Rng &ri, Rng &rp,
+                               uint32_t nblk, uint32_t b0, uint32_t phase, uint32_t lane, uint32_t r, uint32_t &flast,
+                               uint32_t &nc, uint32_t &pick_err_blk, uint32_t &err)
+{
+    uint32_t Icur = draw_interval(ri, lt);
+    uint32_t fcur = wide_pick(rng_next(rp), s.cumw, s.bucket, a.m, a.W, a.mult);
+    uint64_t tsum = 0;
+    nc = 0;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const uint32_t Inext = draw_interval(ri, lt);
+        const uint32_t fnext = wide_pick(rng_next(rp), s.cumw, s.bucket, a.m, a.W, a.mult);
+        tsum += Icur;
+        bool slow = false;
+        if (fcur < a.m) {
+            atomicAdd(&s.hist[fcur], 1u);
+            slow = Inext <= s.fthr[fcur];
+        } else if (pick_err_blk == WIDE_NONE) {
+            pick_err_blk = b0 + b;
+        }
+        if (slow) {
+            const uint32_t c = atomicAdd(s.cc, 1u);
+            if (c < a.rcap) {
+                WideCand e;
+                e.block = b0 + b;
+                e.f = fcur;
+                e.inext = Inext;
+                e.fnext = fnext;
+                e.phase = phase;
+                e.lane_seq = (lane << 16) | nc;
+                e.offset = tsum;
+                e.ri = ri;
+                e.rp = rp;
+                a.cand[(size_t)r * a.rcap + c] = e;
+            } else {
+                err |= WERR_CAND;
+            }
+            ++nc;
+        }
+        flast = fcur;
+        Icur = Inext;
+        fcur = fnext;
+    }
+    return tsum;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- W1
+__global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
+{
+    extern __shared__ uint32_t sh[];
+    __shared__ LogEntry s_log[LOG_TAB];
+    __shared__ uint32_t s_cc[4];
+    const uint32_t m = a.m, tid = threadIdx.x;
+    uint32_t *s_cumw = sh, *s_fthr = sh + m, *s_bkt = sh + 2 * m, *s_hist = sh + 2 * m + WB_N;
+    for (uint32_t i = tid; i < m; i += 256) {
+        s_cumw[i] = a.cumw[i];
+        s_fthr[i] = a.fthr[i];
+    }
+    for (uint32_t i = tid; i < WB_N; i += 256) s_bkt[i] = a.bucket[i];
+    for (uint32_t i = tid; i < 4 * m; i += 256) s_hist[i] = 0;
+    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = a.logt[i];
+    if (tid < 4) s_cc[tid] = 0;
+    __syncthreads();
+
+    const uint32_t w = tid >> 6, lane = tid & 63u;
+    const uint32_t r = blockIdx.x * 4 + w;  // slice-local run
+    if (r >= a.n) return;                   // wave-uniform; no block barrier below
+    const W1Lds s{s_cumw, s_fthr, s_bkt, s_hist + w * m, s_cc + w};
+    const uint64_t run = a.run_begin + r;
+    const Rng ri0 = rng_seed(seed_interval(a.seed_base, run));
+    const Rng rp0 = rng_seed(seed_picker(a.seed_base, run));
+    const int64_t D = a.D;
+    WideLane *lanes = a.lanes + (size_t)r * (1 + a.nch) * 64;
+
+    uint32_t err = 0, pick_err_blk = WIDE_NONE, flast = WIDE_NONE;
+    uint64_t Tph = 0;                  // T of the last block before the phase (T_{-1} = 0)
+    uint32_t fprev = WIDE_NONE;        // finder of that block
+    bool done = false;
+    uint32_t n_end = 0, lastf = WIDE_NONE, nph_run = 0;
+    uint64_t tlast = 0;
+
+    // One phase: lane segments of nblk blocks from draw b0(lane); ri/rp positioned there.
+    auto phase = [&](Rng &ri, Rng &rp, uint32_t nblk, uint32_t b0, uint32_t ph) {
+        const Rng ris = ri, rps = rp;
+        uint32_t nc = 0;
+        flast = fprev;
+        const uint64_t tsum = w1_segment(a, s, s_log, ri, rp, nblk, b0, ph, lane, r, flast, nc, pick_err_blk, err);
+        const uint64_t excl = wave_excl_scan(tsum, lane);
+        const uint64_t t0 = Tph + excl, tend = t0 + tsum;
+        lanes[(size_t)ph * 64 + lane] = WideLane{t0, nc, 0u};
+        nph_run = ph + 1;
+        const uint64_t ge = __ballot(nblk > 0 && (int64_t)tend >= D);
+        if (ge) {
+            // The run ends in this phase: lane L* holds the first block found at >= D.
+            const uint32_t Ls = (uint32_t)__ffsll((unsigned long long)ge) - 1;
+            const uint32_t fprev_lane = __shfl(flast, (int)(Ls == 0 ? 0 : Ls - 1), 64);
+            uint32_t ne = WIDE_NONE, lf = WIDE_NONE;
+            uint64_t tl = 0;
+            if (lane > Ls) {  // every block of the segment is past the end: take them out again
+                Rng p = rps;
+                for (uint32_t b = 0; b < nblk; ++b) {
+                    const uint32_t f = wide_pick(rng_next(p), s.cumw, s.bucket, m, a.W, a.mult);
+                    if (f < m) atomicSub(&s.hist[f], 1u);
+                }
+            } else if (lane == Ls) {
+                Rng i2 = ris, p2 = rps;
+                uint64_t T = t0;
+                lf = Ls == 0 ? fprev : fprev_lane;
+                tl = t0;
+                for (uint32_t b = 0; b < nblk; ++b) {
+                    T += (uint32_t)draw_interval(i2, s_log);
+                    const uint32_t f = wide_pick(rng_next(p2), s.cumw, s.bucket, m, a.W, a.mult);
+                    if ((int64_t)T >= D) {
+                        if (ne == WIDE_NONE) ne = b0 + b;
+                        if (f < m) atomicSub(&s.hist[f], 1u);
+                    } else {
+                        lf = f;
+                        tl = T;
+                    }
+                }
+            }
+            n_end = __shfl(ne, (int)Ls, 64);
+            lastf = __shfl(lf, (int)Ls, 64);
+            tlast = __shfl((unsigned long long)tl, (int)Ls, 64);
+            done = true;
+        } else {
+            Tph += __shfl((unsigned long long)(excl + tsum), 63, 64);
+            fprev = __shfl(flast, 63, 64);
+        }
+    };
+
+    if (a.S0 > 0) {
+        Rng ri = ri0, rp = rp0;
+        jump_both(reinterpret_cast<const uint4 *>(a.jmain) + (size_t)lane * 128, ri, rp);
+        phase(ri, rp, a.S0, lane * a.S0, 0u);
+    } else {
+        lanes[lane] = WideLane{0, 0, 0};
+        nph_run = 1;
+    }
+    if (!done) {
+        Rng ri = ri0, rp = rp0;
+        jump_both(reinterpret_cast<const uint4 *>(a.jtail) + (size_t)lane * 128, ri, rp);
+        for (uint32_t c = 0; c < a.nch && !done; ++c) {
+            const uint32_t b0 = (uint32_t)(a.B0 + (uint64_t)c * 64 * a.ST + (uint64_t)lane * a.ST);
+            phase(ri, rp, a.ST, b0, 1u + c);
+            if (!done && c + 1 < a.nch) jump_both(reinterpret_cast<const uint4 *>(a.jstep), ri, rp);
+        }
+    }
+    if (!done) err |= WERR_DRAWS;
+    for (uint32_t ph = nph_run; ph < 1 + a.nch; ++ph) lanes[(size_t)ph * 64 + lane] = WideLane{0, 0, 0};
+    // A PickFinder fall-through only matters before the end of the run (the reference never draws later).
+    uint32_t pe = pick_err_blk;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(pe, o, 64);
+        pe = y < pe ? y : pe;
+    }
+    if (done && pe != WIDE_NONE && pe < n_end) err |= WERR_PICK;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) err |= __shfl_xor(err, o, 64);
+    wave_sync();
+    uint32_t *hout = a.hist + (size_t)r * m;
+    for (uint32_t k = lane; k < m; k += 64) hout[k] = s.hist[k];
+    if (lane == 0) {
+        const uint32_t cc = *s.cc;
+        uint32_t *inf = a.info + (size_t)r * 4;
+        inf[0] = n_end;
+        inf[1] = lastf;
+        inf[2] = cc < a.rcap ? cc : a.rcap;
+        inf[3] = err;
+        a.tlast[r] = (int64_t)tlast;
+    }
+}
+
+// ---------------------------------------------------------------- W2
+__global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a)
+{
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t r = (uint32_t)(idx / a.rcap), c = (uint32_t)(idx % a.rcap);
+    if (r >= a.n) return;
+    const uint32_t *inf = a.info + (size_t)r * 4;
+    if (c >= inf[2]) return;
+    const WideCand e = a.cand[idx];
+    uint32_t *rec = a.recs + idx * WREC_WORDS;
+    if (inf[3] != 0 || e.block >= inf[0]) {  // failed run, or a block past the end of the run
+        rec[0] = e.block + 1;
+        rec[1] = WREC_SKIP;
+        rec[2] = 0;
+        return;
+    }
+    const WideLane ln = a.lanes[((size_t)r * (1 + a.nch) + e.phase) * 64 + (e.lane_seq >> 16)];
+    const int64_t Ts = (int64_t)(ln.t0 + e.offset);
+    WideSrc src{e.ri, e.rp, a.logt, a.cumw, a.bucket, a.m, a.W, a.mult};
+    WideEpOut o;
+    wide_episode(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
+    rec[0] = o.end;
+    rec[1] = o.flags;
+    rec[2] = o.ne;
+    for (uint32_t i = 0; i < o.ne; ++i) {
+        rec[4 + 3 * i] = o.gid[i];
+        rec[5 + 3 * i] = o.dF[i];
+        rec[6 + 3 * i] = o.dS[i];
+    }
+}
+
+// ---------------------------------------------------------------- W3
+// LDS: acc[m] x {found, stale, share, rate} u64 (workgroup sums), then per wave: hist F[m], stale S[m],
+// sorted candidate keys (block, slot) and their (end, flags), per-(phase, lane) bases.
+__global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a, const WideOut out)
+{
+    extern __shared__ uint64_t sh64[];
+    const uint32_t m = a.m, tid = threadIdx.x, w = tid >> 6, lane = tid & 63u;
+    const uint32_t nph = 1 + a.nch;
+    unsigned long long *acc = (unsigned long long *)sh64;  // [m][4]
+    uint32_t *wbase = (uint32_t *)(sh64 + (size_t)4 * m);
+    const size_t per_wave = (size_t)2 * m + 3 * (size_t)a.rcap + (size_t)nph * 64;
+    uint32_t *F = wbase + w * per_wave, *S = F + m, *KB = S + m, *KE = KB + a.rcap, *KF = KE + a.rcap,
+             *base = KF + a.rcap;
+    for (uint32_t i = tid; i < 4 * m; i += 256) acc[i] = 0;
+    __syncthreads();
+    const int64_t D = a.D;
+    for (uint32_t r = blockIdx.x * 4 + w; r < a.n; r += gridDim.x * 4) {  // wave-uniform loop
+        const uint32_t *inf = a.info + (size_t)r * 4;
+        const uint32_t n_end = inf[0], lastf = inf[1], cc = inf[2], rerr = inf[3];
+        bool ok = rerr == 0;
+        for (uint32_t k = lane; k < m; k += 64) {
+            F[k] = a.hist[(size_t)r * m + k];
+            S[k] = 0;
+        }
+        // sorted position of every candidate: (phase, lane) base + rank within the lane
+        const WideLane *lanes = a.lanes + (size_t)r * nph * 64;
+        uint32_t run_total = 0;
+        for (uint32_t ph = 0; ph < nph; ++ph) {
+            const uint32_t cnt = lanes[(size_t)ph * 64 + lane].count;
+            const uint32_t ex = (uint32_t)wave_excl_scan(cnt, lane);
+            base[ph * 64 + lane] = run_total + ex;
+            run_total += __shfl(ex + cnt, 63, 64);
+        }
+        if (run_total != cc) ok = false;  // overflowed list (also flagged by W1)
+        wave_sync();
+        if (ok) {
+            for (uint32_t c = lane; c < cc; c += 64) {
+                const WideCand &e = a.cand[(size_t)r * a.rcap + c];
+                const uint32_t pos = base[e.phase * 64 + (e.lane_seq >> 16)] + (e.lane_seq & 0xFFFFu);
+                const uint32_t *rec = a.recs + ((size_t)r * a.rcap + c) * WREC_WORDS;
+                if (pos < cc) {
+                    KB[pos] = e.block;
+                    KE[pos] = rec[0];
+                    KF[pos] = (rec[1] << 16) | c;
+                }
+            }
+        }
+        wave_sync();
+        // chain the episodes whose first block is reached quiet (serial over the sorted list)
+        uint32_t cursor = 0;
+        bool run_ended = false;
+        if (ok) {
+            for (uint32_t i = 0; i < cc; ++i) {
+                const uint32_t sblk = KB[i];
+                if (sblk >= n_end) break;
+                if (sblk < cursor) continue;
+                const uint32_t fl = KF[i] >> 16, c = KF[i] & 0xFFFFu;
+                if (fl & (WREC_ERR | WREC_SKIP)) {
+                    ok = false;
+                    break;
+                }
+                const uint32_t *rec = a.recs + ((size_t)r * a.rcap + c) * WREC_WORDS;
+                const uint32_t ne = rec[2];
+                if (lane < ne) {
+                    const uint32_t g = rec[4 + 3 * lane];
+                    F[g] += rec[5 + 3 * lane];
+                    S[g] += rec[6 + 3 * lane];
+                }
+                wave_sync();
+                cursor = KE[i];
+                if (fl & WREC_ENDED) {
+                    run_ended = true;
+                    break;
+                }
+            }
+        }
+        // the run ended quiet and its last block was fast: it counts only if it arrived by D (main.cpp:185)
+        if (ok && lane == 0 && !run_ended && n_end > 0 && cursor < n_end && lastf < m) {
+            if (a.tlast[r] + a.prop[lastf] > D) F[lastf] -= 1u;
+        }
+        wave_sync();
+        if (!ok) {
+            if (lane == 0) atomicAdd(out.fail, 1u);
+            continue;
+        }
+        uint32_t Lp = 0;
+        for (uint32_t k = lane; k < m; k += 64) Lp += F[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) Lp += __shfl_xor(Lp, o, 64);
+        const double Ld = (double)Lp;  // |best chain| - 1 (main.cpp:28)
+        const uint32_t rel = out.rel_begin + r;
+        for (uint32_t k = lane; k < m; k += 64) {
+            const uint32_t f = F[k], st = S[k];
+            if (out.records) {
+                out.records[2 * ((size_t)rel * m + k) + 0] = f;
+                out.records[2 * ((size_t)rel * m + k) + 1] = st;
+            }
+            if (f == 0 && st == 0) continue;
+            // MinerStats (main.cpp:28-29) as Q32.32 fixed point
+            const double share = f == 0 ? 0.0 : (double)f / Ld;
+            const double rate = f == 0 ? 0.0 : (double)st / (double)f;
+            const uint64_t sfx = (uint64_t)(share * 4294967296.0 + 0.5);
+            const uint64_t rfx = (uint64_t)(rate * 4294967296.0 + 0.5);
+            atomicAdd(&acc[4 * k + 0], (unsigned long long)f);
+            atomicAdd(&acc[4 * k + 1], (unsigned long long)st);
+            atomicAdd(&acc[4 * k + 2], (unsigned long long)sfx);
+            atomicAdd(&acc[4 * k + 3], (unsigned long long)rfx);
+        }
+        if (out.best_h && lane == 0) out.best_h[rel] = Lp;
+    }
+    __syncthreads();
+    // flush: msim_sums {found, stale, share_hi, share_lo, rate_hi, rate_lo}; the workgroup's Q32.32 sums
+    // are split into 2^32 and 2^0 limbs (the represented value sum(hi) + sum(lo) * 2^-32 is exact).
+    for (uint32_t k = tid; k < m; k += 256) {
+        const unsigned long long *x = acc + 4 * k;
+        unsigned long long *o = (unsigned long long *)out.sums + 6 * k;
+        if (x[0]) atomicAdd(o + 0, x[0]);
+        if (x[1]) atomicAdd(o + 1, x[1]);
+        if (x[2]) {
+            atomicAdd(o + 2, x[2] >> 32);
+            atomicAdd(o + 3, x[2] & 0xFFFFFFFFull);
+        }
+        if (x[3]) {
+            atomicAdd(o + 4, x[3] >> 32);
+            atomicAdd(o + 5, x[3] & 0xFFFFFFFFull);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- weighted pick (test surface)
+__global__ void msim_wide_pick_kernel(const uint32_t *__restrict__ cumw, const uint32_t *__restrict__ bucket, uint32_t m,
+                                      uint32_t W, uint64_t mult, const uint64_t *__restrict__ u, int32_t *__restrict__ out,
+                                      uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = wide_pick(u[i], cumw, bucket, m, W, mult);
+    out[i] = k >= m ? -1 : (int32_t)k;
+}
+
+// ---------------------------------------------------------------- host side
+size_t wide_w1_lds(uint32_t m) { return ((size_t)2 * m + WB_N + 4 * (size_t)m) * 4; }
+size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch)
+{
+    return (size_t)4 * m * 8 + 4 * ((size_t)2 * m + 3 * (size_t)rcap + (size_t)(1 + nch) * 64) * 4;
+}
+
+hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, const WideOut &out, hipStream_t s,
+                       std::vector<hipEvent_t> *w1_events)
+{
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)msim_wide_draws_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)wide_w1_lds(WIDE_MAX_M));
+        (void)hipFuncSetAttribute((const void *)msim_wide_combine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_done = true;
+    }
+    WideArgs a = proto;
+    a.hist = (uint32_t *)(ws + L.hist_off);
+    a.info = (uint32_t *)(ws + L.info_off);
+    a.tlast = (int64_t *)(ws + L.tlast_off);
+    a.lanes = (WideLane *)(ws + L.lanes_off);
+    a.cand = (WideCand *)(ws + L.cand_off);
+    a.recs = (uint32_t *)(ws + L.recs_off);
+    const size_t l1 = wide_w1_lds(a.m), l3 = wide_w3_lds(a.m, a.rcap, a.nch);
+    if (l3 > 160 * 1024) return hipErrorInvalidValue;
+    for (uint64_t off = 0; off < out.n_total; off += L.nr) {
+        const uint32_t cn = (uint32_t)((out.n_total - off) < L.nr ? (out.n_total - off) : L.nr);
+        a.run_begin = out.run_begin + off;
+        a.n = cn;
+        hipEvent_t eb = nullptr, ee = nullptr;
+        if (w1_events && hipEventCreate(&eb) == hipSuccess && hipEventCreate(&ee) == hipSuccess) {
+            w1_events->push_back(eb);
+            w1_events->push_back(ee);
+            (void)hipEventRecord(eb, s);
+        }
+        hipLaunchKernelGGL(msim_wide_draws_kernel, dim3((cn + 3) / 4), dim3(256), l1, s, a);
+        if (ee) (void)hipEventRecord(ee, s);
+        const size_t nthreads = (size_t)cn * a.rcap;
+        hipLaunchKernelGGL(msim_wide_episode_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a);
+        WideOut o = out;
+        o.rel_begin = (uint32_t)off;
+        uint32_t g3 = (cn + 3) / 4;
+        if (g3 > 4096) g3 = 4096;
+        hipLaunchKernelGGL(msim_wide_combine_kernel, dim3(g3), dim3(256), l3, s, a, o);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_picks(const WideArgs &a, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(msim_wide_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.cumw, a.bucket, a.m,
+                       a.W, a.mult, u, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace msim

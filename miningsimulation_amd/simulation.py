@@ -58,6 +58,19 @@ PRESETS = {
     "c3": lambda: setup_miners(1_000, selfish_perc=40),
     "default": lambda: setup_miners(1_000),
 }
+C5_TOTAL_WEIGHT = 102_400
+
+
+def c5_network(propagation_ms: int = 1000) -> List[Miner]:
+    """BASELINE.json configs[4]: 2 pools + 1024 small miners, integer weights summing to
+    W = 102400 (pool 0 30%, pool 1 29%, 1024 x 41 = 41%), all honest. Not expressible in the reference
+    (integer percentages summing to 100, main.cpp:43); run with Simulation(..., total_weight=C5_TOTAL_WEIGHT)."""
+    w = [30720, 29696] + [41] * 1024
+    return [Miner(k, x, propagation_ms) for k, x in enumerate(w)]
+
+
+PRESET_WEIGHTS = {"c5": C5_TOTAL_WEIGHT}
+PRESETS["c5"] = c5_network
 C4_SELFISH_PERCS = list(range(10, 50))
 C4_PROPAGATIONS_MS = [100, 250, 500, 1000, 2000, 5000, 10000, 20000, 30000]
 
@@ -103,13 +116,25 @@ def _miners_struct(miners: Sequence[Miner]):
 class Simulation:
     """A network description bound to the device library (msim_config)."""
 
-    def __init__(self, miners: Sequence[Miner], duration_ms: int = SIM_DURATION_MS):
+    def __init__(self, miners: Sequence[Miner], duration_ms: int = SIM_DURATION_MS, total_weight: int = 100):
+        """total_weight = 100: Miner.perc are the reference's integer percentages (SetupMiners, main.cpp:43).
+        Otherwise Miner.perc are integer weights summing to total_weight."""
         self.miners = list(miners)
         self.duration_ms = int(duration_ms)
+        self.total_weight = int(total_weight)
         handle = ctypes.c_void_p()
-        check(lib.msim_config_create(_miners_struct(self.miners), len(self.miners), self.duration_ms,
-                                     ctypes.byref(handle)), "msim_config_create")
+        if self.total_weight == 100:
+            check(lib.msim_config_create(_miners_struct(self.miners), len(self.miners), self.duration_ms,
+                                         ctypes.byref(handle)), "msim_config_create")
+        else:
+            check(lib.msim_config_create_weighted(_miners_struct(self.miners), len(self.miners), self.duration_ms,
+                                                  self.total_weight, ctypes.byref(handle)), "msim_config_create_weighted")
         self._h = handle
+
+    @property
+    def wide(self) -> bool:
+        """True when the network runs on the large-network pipeline (msim_wide.h)."""
+        return bool(lib.msim_config_is_wide(self._h))
 
     @property
     def handle(self) -> ctypes.c_void_p:

@@ -99,9 +99,16 @@ int64_t oracle_next_block_interval(oracle_rng *r)
  * Returns the miner INDEX, or -1 where the reference would hit its assert (simulation.h:220). */
 int oracle_pick_finder(const uint64_t *perc, int n, oracle_rng *r)
 {
+    return oracle_pick_finder_w(perc, n, OR_PERC_MULTIPLIER, r);
+}
+
+/* SURVEY Appendix C weight generalisation (configs[4], not expressible in the reference): integer
+ * weights summing to W, multiplier UINT64_MAX / W. With W = 100 this is exactly simulation.h:18,217. */
+int oracle_pick_finder_w(const uint64_t *perc, int n, uint64_t mult, oracle_rng *r)
+{
     uint64_t random = oracle_rng_rand64(r), i = 0;
     for (int k = 0; k < n; ++k) {
-        i += perc[k] * OR_PERC_MULTIPLIER;
+        i += perc[k] * mult;
         if (i > random) return k;
     }
     return -1;
@@ -283,7 +290,15 @@ static int or_earliest_arrival(const or_miner *ms, int n, int64_t t, int64_t *ou
 int oracle_run(const oracle_miner *miners, int n, int64_t duration_ms, uint32_t seed_interval,
                uint32_t seed_picker, oracle_run_stats *out, oracle_trace *trace)
 {
-    if (n <= 0) return ORACLE_EINVAL;
+    return oracle_run_w(miners, n, duration_ms, 100u, seed_interval, seed_picker, out, trace);
+}
+
+/* RunSimulation with the Appendix C weight generalisation: perc holds integer weights, total_weight = W. */
+int oracle_run_w(const oracle_miner *miners, int n, int64_t duration_ms, uint64_t total_weight,
+                 uint32_t seed_interval, uint32_t seed_picker, oracle_run_stats *out, oracle_trace *trace)
+{
+    if (n <= 0 || total_weight == 0) return ORACLE_EINVAL;
+    const uint64_t mult = UINT64_MAX / total_weight;
     or_miner *ms = (or_miner *)calloc((size_t)n, sizeof(or_miner));
     uint64_t *perc = (uint64_t *)calloc((size_t)n, sizeof(uint64_t));
     for (int k = 0; k < n; ++k) {
@@ -302,7 +317,7 @@ int oracle_run(const oracle_miner *miners, int n, int64_t duration_ms, uint32_t 
     for (int64_t cur_time = 0; cur_time < duration_ms;) {
         events++;
         while (cur_time == next_block_time) { /* main.cpp:153-157 */
-            const int k = oracle_pick_finder(perc, n, &miner_picker);
+            const int k = oracle_pick_finder_w(perc, n, mult, &miner_picker);
             if (k < 0) { rc = ORACLE_EPICK; goto done; }
             or_found_block(&ms[k], next_block_time, best_chain_size);
             next_block_time += oracle_next_block_interval(&block_interval);
@@ -352,6 +367,7 @@ typedef struct {
     const oracle_miner *miners;
     int n;
     int64_t duration_ms;
+    uint64_t total_weight;
     uint64_t run_begin, n_runs;
     uint32_t seed_base;
     int nthreads, tid;
@@ -369,7 +385,7 @@ static void *or_worker(void *arg)
         const uint32_t si = (uint32_t)(j->seed_base + 2u * run);
         const uint32_t sp = (uint32_t)(j->seed_base + 2u * run + 1u);
         oracle_run_stats *o = j->per_run ? &j->per_run[r * (uint64_t)j->n] : tmp;
-        int rc = oracle_run(j->miners, j->n, j->duration_ms, si, sp, o, NULL);
+        int rc = oracle_run_w(j->miners, j->n, j->duration_ms, j->total_weight, si, sp, o, NULL);
         if (rc) { j->rc = rc; break; }
     }
     free(tmp);
@@ -380,18 +396,26 @@ int oracle_run_batch(const oracle_miner *miners, int n, int64_t duration_ms, uin
                      uint64_t n_runs, uint32_t seed_base, int nthreads, oracle_run_stats *per_run,
                      oracle_stats_sum *sums)
 {
+    return oracle_run_batch_w(miners, n, duration_ms, 100u, run_begin, n_runs, seed_base, nthreads, per_run, sums);
+}
+
+int oracle_run_batch_w(const oracle_miner *miners, int n, int64_t duration_ms, uint64_t total_weight,
+                       uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, int nthreads,
+                       oracle_run_stats *per_run, oracle_stats_sum *sums)
+{
     if (nthreads < 1) nthreads = 1;
     if (!per_run && sums) {
         /* sums need per-run values in run order; allocate internally. */
         per_run = (oracle_run_stats *)calloc(n_runs * (uint64_t)n, sizeof(oracle_run_stats));
-        int rc = oracle_run_batch(miners, n, duration_ms, run_begin, n_runs, seed_base, nthreads, per_run, sums);
+        int rc = oracle_run_batch_w(miners, n, duration_ms, total_weight, run_begin, n_runs, seed_base, nthreads,
+                                    per_run, sums);
         free(per_run);
         return rc;
     }
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     or_job *jobs = (or_job *)calloc((size_t)nthreads, sizeof(or_job));
     for (int t = 0; t < nthreads; ++t) {
-        jobs[t] = (or_job){miners, n, duration_ms, run_begin, n_runs, seed_base, nthreads, t, per_run, 0};
+        jobs[t] = (or_job){miners, n, duration_ms, total_weight, run_begin, n_runs, seed_base, nthreads, t, per_run, 0};
         pthread_create(&th[t], NULL, or_worker, &jobs[t]);
     }
     int rc = 0;

@@ -46,6 +46,12 @@ uint64_t oracle_rng_rand64(oracle_rng *r);
 double oracle_exporand(oracle_rng *r, double mean);
 int64_t oracle_next_block_interval(oracle_rng *r);
 int oracle_pick_finder(const uint64_t *perc, int n, oracle_rng *r);
+int oracle_pick_finder_w(const uint64_t *perc, int n, uint64_t mult, oracle_rng *r);
+int oracle_run_w(const oracle_miner *miners, int n, int64_t duration_ms, uint64_t total_weight,
+                 uint32_t seed_interval, uint32_t seed_picker, oracle_run_stats *out, oracle_trace *trace);
+int oracle_run_batch_w(const oracle_miner *miners, int n, int64_t duration_ms, uint64_t total_weight,
+                       uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, int nthreads,
+                       oracle_run_stats *per_run, oracle_stats_sum *sums);
 
 int oracle_run(const oracle_miner *miners, int n, int64_t duration_ms, uint32_t seed_interval,
                uint32_t seed_picker, oracle_run_stats *out, oracle_trace *trace);

@@ -4,7 +4,7 @@
  *   oracle_cli kat                      print SURVEY Appendix B known-answer values
  *   oracle_cli hash PROP_MS RUNS        FNV-1a-64 over per-run {found, bits(share), bits(stale_rate)}
  *   oracle_cli time PRESET RUNS THREADS time RUNS run-years of a preset on THREADS threads
- *                                        (PRESET: c1 | c2 | c3 | default)
+ *                                        (PRESET: c1 | c2 | c3 | c5 | default)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -15,8 +15,22 @@
 
 #define MONTHS12_MS 31556952000LL /* main.cpp:7 SIM_DURATION = months{12} */
 
-static void preset(const char *name, oracle_miner *m, int *n)
+#define C5_M 1026
+#define C5_W 102400u
+
+/* SURVEY Appendix C (BASELINE configs[4]): pools 30720, 29696 and 1024 miners of weight 41, W = 102400. */
+static uint64_t preset(const char *name, oracle_miner *m, int *n)
 {
+    if (!strcmp(name, "c5")) {
+        *n = C5_M;
+        for (int k = 0; k < C5_M; ++k) {
+            m[k].id = (uint32_t)k;
+            m[k].perc = k == 0 ? 30720u : (k == 1 ? 29696u : 41u);
+            m[k].propagation_ms = 1000;
+            m[k].is_selfish = 0;
+        }
+        return C5_W;
+    }
     static const uint64_t honest[9] = {30, 29, 12, 11, 8, 5, 3, 1, 1};
     static const uint64_t selfish[9] = {40, 19, 12, 11, 8, 5, 3, 1, 1};
     int64_t prop = 1000;
@@ -32,6 +46,7 @@ static void preset(const char *name, oracle_miner *m, int *n)
         m[k].propagation_ms = prop;
         m[k].is_selfish = (k == 0) ? s0 : 0;
     }
+    return 100u;
 }
 
 static uint64_t fnv(uint64_t h, uint64_t w) { return (h ^ w) * 0x100000001b3ULL; }
@@ -88,21 +103,21 @@ int main(int argc, char **argv)
         return 0;
     }
     if (!strcmp(argv[1], "time") && argc >= 5) {
-        oracle_miner m[9];
+        static oracle_miner m[C5_M];
         int n;
-        preset(argv[2], m, &n);
+        const uint64_t W = preset(argv[2], m, &n);
         const uint64_t runs = strtoull(argv[3], NULL, 10);
         const int threads = atoi(argv[4]);
-        oracle_stats_sum sums[9];
+        static oracle_stats_sum sums[C5_M];
         struct timespec a, b;
         clock_gettime(CLOCK_MONOTONIC, &a);
-        int rc = oracle_run_batch(m, n, MONTHS12_MS, 0, runs, 1000, threads, NULL, sums);
+        int rc = oracle_run_batch_w(m, n, MONTHS12_MS, W, 0, runs, 1000, threads, NULL, sums);
         clock_gettime(CLOCK_MONOTONIC, &b);
         if (rc) { fprintf(stderr, "rc=%d\n", rc); return 1; }
         const double dt = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
         printf("{\"preset\": \"%s\", \"runs\": %llu, \"threads\": %d, \"seconds\": %.4f, \"run_years_per_s\": %.3f}\n",
                argv[2], (unsigned long long)runs, threads, dt, (double)runs / dt);
-        for (int k = 0; k < n; ++k)
+        for (int k = 0; k < n && k < 9; ++k)
             printf("  miner %d: found %lld share %.6g%% stale %.6g%%\n", k, (long long)(sums[k].blocks_found / (int64_t)runs),
                    sums[k].blocks_share * 100 / (double)runs, sums[k].stale_rate * 100 / (double)runs);
         return 0;

@@ -57,6 +57,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_run_batch.argtypes = [ctypes.POINTER(OMiner), ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
                                        ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ORunStats),
                                        ctypes.POINTER(OSum)]
+        L.oracle_run_batch_w.argtypes = [ctypes.POINTER(OMiner), ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.POINTER(ORunStats), ctypes.POINTER(OSum)]
+        L.oracle_pick_finder_w.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_uint64,
+                                           ctypes.POINTER(ORng)]
         L.oracle_rng_seed.argtypes = [ctypes.POINTER(ORng), ctypes.c_uint64]
         L.oracle_rng_rand64.argtypes = [ctypes.POINTER(ORng)]
         L.oracle_rng_rand64.restype = ctypes.c_uint64
@@ -103,14 +108,15 @@ def run(percs, props, selfish, duration_ms: int, seed_interval: int, seed_picker
 
 
 def run_batch(percs, props, selfish, duration_ms: int, n_runs: int, run_begin: int = 0, seed_base: int = 1000,
-              threads: int = 8):
+              threads: int = 8, total_weight: int = 100):
     """Per-run stats for runs [run_begin, run_begin+n) with the SURVEY seed convention.
 
+    total_weight != 100: `percs` are integer weights summing to it (SURVEY Appendix C generalisation).
     Returns (found [n, M] int64, stale [n, M] int64, share [n, M] f64, rate [n, M] f64)."""
     m = len(percs)
     out = (ORunStats * (n_runs * m))()
-    rc = lib().oracle_run_batch(_miners(percs, props, selfish), m, duration_ms, run_begin, n_runs,
-                                seed_base & 0xFFFFFFFF, threads, out, None)
+    rc = lib().oracle_run_batch_w(_miners(percs, props, selfish), m, duration_ms, total_weight, run_begin, n_runs,
+                                  seed_base & 0xFFFFFFFF, threads, out, None)
     if rc:
         raise RuntimeError(f"oracle_run_batch rc={rc}")
     a = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), shape=(n_runs * m * 32,))
@@ -136,6 +142,15 @@ def picks(percs: Sequence[int], seed: int, n: int) -> List[int]:
     lib().oracle_rng_seed(ctypes.byref(r), seed)
     P = (ctypes.c_uint64 * len(percs))(*percs)
     return [lib().oracle_pick_finder(P, len(percs), ctypes.byref(r)) for _ in range(n)]
+
+
+def picks_w(weights: Sequence[int], total_weight: int, seed: int, n: int) -> List[int]:
+    """PickFinder with the Appendix C weight generalisation (multiplier UINT64_MAX // W)."""
+    r = ORng()
+    lib().oracle_rng_seed(ctypes.byref(r), seed)
+    P = (ctypes.c_uint64 * len(weights))(*weights)
+    mult = 0xFFFFFFFFFFFFFFFF // total_weight
+    return [lib().oracle_pick_finder_w(P, len(weights), mult, ctypes.byref(r)) for _ in range(n)]
 
 
 def log1p_array(x: np.ndarray) -> np.ndarray:

@@ -34,9 +34,10 @@ def native_tests():
     lib = os.path.join(ROOT, "build", "libmodel_host.so")
     pipe = os.path.join(ROOT, "build", "libpipeline_host.so")
     chk = os.path.join(ROOT, "build", "draws_check")
-    if not (os.path.exists(lib) and os.path.exists(chk) and os.path.exists(pipe)):
+    wide = os.path.join(ROOT, "build", "libwide_host.so")
+    if not all(os.path.exists(p) for p in (lib, chk, pipe, wide)):
         ge.build_native_tests()
-    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe}
+    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide}
 
 
 @pytest.fixture(scope="session")

@@ -47,7 +47,8 @@ def test_config_validation_without_gpu(msim_lib_path):
         ([Miner(0, 60, 1000), Miner(1, 50, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 110
         ([Miner(0, 50, 1000, True), Miner(1, 50, 1000, True)], _lib.MSIM_E_SELFISH),
         ([Miner(0, 50, 1000), Miner(0, 50, 1000)], _lib.MSIM_E_MINERS),             # duplicate id
-        ([Miner(k, 6 if k < 10 else 5, 1000) for k in range(16)], _lib.MSIM_E_MINERS),
+        ([Miner(k, 7 if k < 10 else 5, 1000, k == 0) for k in range(16)], _lib.MSIM_E_SELFISH),  # wide: honest only
+        ([Miner(k, 1 if k < 100 else 0, 1000) for k in range(4097)], _lib.MSIM_E_MINERS),
         ([Miner(0, 50, -1), Miner(1, 50, 1000)], _lib.MSIM_E_INVALID),
     ]
     for miners, code in bad:
@@ -57,6 +58,22 @@ def test_config_validation_without_gpu(msim_lib_path):
             assert e.code == code, (miners, e)
         else:
             raise AssertionError(f"accepted invalid network {miners}")
+    # the large-network path (msim_wide.h): more than 15 honest miners, or integer weights
+    assert Simulation([Miner(k, 7 if k < 10 else 5, 1000) for k in range(16)]).wide
+    assert not Simulation(setup_miners()).wide
+    c5 = [Miner(k, w, 1000) for k, w in enumerate([30720, 29696] + [41] * 1024)]
+    assert Simulation(c5, total_weight=102400).wide
+    for miners, W, code in (
+        (c5, 102401, _lib.MSIM_E_WEIGHTS),                                      # weights sum to 102400
+        ([Miner(0, 1 << 31, 1000)], 1 << 31, _lib.MSIM_E_WEIGHTS),              # W >= 2^31
+        ([Miner(0, 7, 1000, True), Miner(1, 3, 1000)], 10, _lib.MSIM_E_SELFISH),  # weighted: honest only
+    ):
+        try:
+            Simulation(miners, total_weight=W)
+        except MsimError as e:
+            assert e.code == code, (W, e)
+        else:
+            raise AssertionError(f"accepted invalid weighted network (W={W})")
 
 
 def test_report_format():
