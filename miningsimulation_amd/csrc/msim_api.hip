@@ -210,8 +210,8 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
     if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
     const uint32_t m = c->n;
     const WideGeom g = wide_geom(c->p.duration_ms);
-    const size_t o_cumw = 0, o_bkt = o_cumw + 4 * (size_t)m, o_fthr = o_bkt + 4 * (size_t)WB_N;
-    const size_t o_prop = (o_fthr + 4 * (size_t)m + 7) / 8 * 8, o_log = o_prop + 8 * (size_t)m;
+    const size_t o_cf = 0, o_bkt = o_cf + 8 * ((size_t)m + 1), o_prop = (o_bkt + 2 * (size_t)WB_N + 7) / 8 * 8;
+    const size_t o_log = o_prop + 8 * (size_t)m;
     const size_t o_jm = (o_log + LOG_TAB * sizeof(LogEntry) + 255) / 256 * 256, o_jt = o_jm + 64 * 2048,
                  o_js = o_jt + 64 * 2048, total = o_js + 2048;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -220,13 +220,13 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
         if (t.first == dev) d = t.second;
     if (!d) {
         std::vector<char> h(total, 0);
-        build_wide_pick(c->wperc.data(), m, (uint32_t)c->total_weight, (uint32_t *)(h.data() + o_cumw),
-                        (uint32_t *)(h.data() + o_bkt));
+        std::vector<uint32_t> fthr(m);
         for (uint32_t k = 0; k < m; ++k) {
-            ((uint32_t *)(h.data() + o_fthr))[k] =
-                c->wprop[k] < (int64_t)FTHR_NEVER ? (uint32_t)c->wprop[k] : FTHR_NEVER;
+            fthr[k] = c->wprop[k] < (int64_t)FTHR_NEVER ? (uint32_t)c->wprop[k] : FTHR_NEVER;
             ((int64_t *)(h.data() + o_prop))[k] = c->wprop[k];
         }
+        build_wide_pick(c->wperc.data(), fthr.data(), m, (uint32_t)c->total_weight, (uint64_t *)(h.data() + o_cf),
+                        (uint16_t *)(h.data() + o_bkt));
         build_log_table((LogEntry *)(h.data() + o_log));
         // jmain[l] = T^(l*S0); jtail[l] = T^(B0 + l*ST); jstep = T^(63*ST - 1)
         auto store = [](const Mat128 &mm, uint32_t *w) {
@@ -258,9 +258,8 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
         c->wtables.push_back({dev, d});
     }
     const char *b = (const char *)d;
-    a->cumw = (const uint32_t *)(b + o_cumw);
-    a->bucket = (const uint32_t *)(b + o_bkt);
-    a->fthr = (const uint32_t *)(b + o_fthr);
+    a->cf = (const uint64_t *)(b + o_cf);
+    a->bucket = (const uint16_t *)(b + o_bkt);
     a->prop = (const int64_t *)(b + o_prop);
     a->logt = (const LogEntry *)(b + o_log);
     a->jmain = (const uint32_t *)(b + o_jm);

@@ -42,12 +42,13 @@
 
 namespace msim {
 
-constexpr uint32_t WIDE_MAX_M = 4096;   // LDS histogram of 4 waves: 64 KiB
-constexpr int WB_BITS = 10;
+constexpr uint32_t WIDE_MAX_M = 4096;   // LDS histogram of 4 waves: 64 KiB; bucket entries are u16
+constexpr int WB_BITS = 12;
 constexpr uint32_t WB_N = 1u << WB_BITS;  // pick buckets
 constexpr uint32_t WIDE_ST = 16;        // tail blocks per lane per chunk
-constexpr int WE = 48;                  // episode block capacity
-constexpr int WA = 16;                  // episode capacity of miners that found a block
+constexpr int WE_FAST = 12, WA_FAST = 6;  // episode capacities (blocks, miners that found one): first pass
+constexpr int WE = 48;                     // ... retry pass (the record format holds WA entries)
+constexpr int WA = 16;
 constexpr uint32_t WREC_WORDS = 4 + 3 * WA;
 constexpr uint32_t WIDE_NONE = 0xFFFFFFFFu;
 
@@ -57,7 +58,7 @@ enum : uint32_t {
     WERR_DRAWS = 4u,  // the run outlasted the pre-planned tail chunks
     WERR_EP = 8u,     // an episode exceeded WE blocks / WA miners
 };
-enum : uint32_t { WREC_ENDED = 1u, WREC_ERR = 2u, WREC_SKIP = 4u };
+enum : uint32_t { WREC_ENDED = 1u, WREC_ERR = 2u, WREC_SKIP = 4u, WREC_RETRY = 8u };
 
 // One non-fast block of a run, with everything an episode needs to replay the run from there.
 struct WideCand {
@@ -79,43 +80,43 @@ struct WideLane {
     uint32_t pad;
 };
 
-// Pick tables of a weighted network (device or host memory).
-struct WidePick {
-    const uint32_t *cumw;    // [m] cumulative weights
-    const uint32_t *bucket;  // [WB_N] first miner whose range can contain q for u in the bucket
-    uint32_t m, W;
-    uint64_t mult;           // (2^64 - 1) / W
-};
-
-MSIM_HD uint32_t wide_pick(uint64_t u, const uint32_t *__restrict__ cumw, const uint32_t *__restrict__ bucket,
-                           uint32_t m, uint32_t W, uint64_t mult)
+// Pick table entry k (k = 0..m; entry m is a sentinel): cumulative weight of miners 0..k in the low
+// word, the fast threshold of miner k (its propagation, clamped to FTHR_NEVER) in the high word, so
+// the scan's last load also yields the finder's threshold. Sentinel: cumulative 0xFFFFFFFF > any q.
+MSIM_HD uint32_t wide_pick(uint64_t u, const uint64_t *__restrict__ cf, const uint16_t *__restrict__ bucket,
+                           uint32_t W, uint64_t mult, uint32_t &fthr)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint64_t p1 = __umul64hi(u, (uint64_t)W);
 #else
     const uint64_t p1 = (uint64_t)(((unsigned __int128)u * W) >> 64);
 #endif
-    const uint64_t q = u >= (p1 + 1) * mult ? p1 + 1 : p1;
+    const uint32_t q = (uint32_t)(u >= (p1 + 1) * mult ? p1 + 1 : p1);
     uint32_t k = bucket[u >> (64 - WB_BITS)];
-    while (k < m && (uint64_t)cumw[k] <= q) ++k;
+    uint64_t e = cf[k];
+    while ((uint32_t)e <= q) e = cf[++k];
+    fthr = (uint32_t)(e >> 32);
     return k;  // == m: fell through (the reference asserts, simulation.h:220)
 }
 
 // ---------------------------------------------------------------- host table builders
-// weights: m integer weights summing to W (validated by the caller, W < 2^32).
-inline void build_wide_pick(const uint64_t *w, uint32_t m, uint32_t W, uint32_t *cumw, uint32_t *bucket)
+// weights: m integer weights summing to W (validated by the caller, W < 2^31); fthr: m thresholds.
+// cf: m + 1 entries; bucket: WB_N entries = first miner whose range can contain q for u in the bucket.
+inline void build_wide_pick(const uint64_t *w, const uint32_t *fthr, uint32_t m, uint32_t W, uint64_t *cf,
+                            uint16_t *bucket)
 {
     uint64_t c = 0;
     for (uint32_t k = 0; k < m; ++k) {
         c += w[k];
-        cumw[k] = (uint32_t)c;
+        cf[k] = (uint64_t)(uint32_t)c | ((uint64_t)fthr[k] << 32);
     }
+    cf[m] = 0xFFFFFFFFull;
     const uint64_t mult = 0xFFFFFFFFFFFFFFFFull / W;
     uint32_t k = 0;
     for (uint32_t b = 0; b < WB_N; ++b) {
         const uint64_t qlo = ((uint64_t)b << (64 - WB_BITS)) / mult;
-        while (k < m && (uint64_t)cumw[k] <= qlo) ++k;
-        bucket[b] = k;
+        while (k < m && (uint32_t)cf[k] <= qlo) ++k;
+        bucket[b] = (uint16_t)k;
     }
 }
 
@@ -144,13 +145,15 @@ inline WideGeom wide_geom(int64_t duration_ms)
 struct WideSrc {
     Rng ri, rp;
     const LogEntry *lt;
-    const uint32_t *cumw, *bucket;
-    uint32_t m, W;
+    const uint64_t *cf;
+    const uint16_t *bucket;
+    uint32_t W;
     uint64_t mult;
     MSIM_HD void next(uint32_t &I, uint32_t &f)
     {
         I = draw_interval(ri, lt);
-        f = wide_pick(rng_next(rp), cumw, bucket, m, W, mult);
+        uint32_t th;
+        f = wide_pick(rng_next(rp), cf, bucket, W, mult, th);
     }
 };
 
@@ -174,17 +177,21 @@ struct WideEpOut {
 // equal, see the same BestChain and apply the same MaybeReorg (simulation.h:124-142), and hold only
 // published blocks; in BestChain (main.cpp:68-82, index order, strict comparisons) they act as one
 // candidate at the position of the lowest passive index.
-template <class Src>
+// CE / CA: capacities of this instantiation; exceeding one sets WREC_RETRY (recompute with larger ones)
+// instead of WREC_ERR.
+template <int CE, int CA, class Src>
 MSIM_HDN void wide_episode(const int64_t *__restrict__ prop, uint32_t m, int64_t D, uint32_t s, int64_t Ts,
                            uint32_t fs, uint32_t inext, uint32_t fnext, Src &src, WideEpOut &o)
 {
-    int32_t par[WE];
-    uint32_t own[WE];
-    int64_t arr[WE];
-    int32_t hgt[WE];
-    uint32_t gid[WA];  // active miners, sorted by index
-    int32_t tip[WA];
-    uint32_t stl[WA], nf[WA];
+    static_assert(CA <= WA, "record holds WA entries");
+    int32_t par[CE];
+    uint32_t own[CE];
+    int64_t arr[CE];
+    int32_t hgt[CE];
+    uint32_t gid[CA];  // active miners, sorted by index
+    int32_t tip[CA];
+    uint32_t stl[CA], nf[CA];
+    uint32_t cap = 0;
     int na = 0, nb = 0, ptip = -1;
     uint32_t err = 0, consumed = 0;
     int64_t Tn = Ts;
@@ -211,8 +218,8 @@ MSIM_HDN void wide_episode(const int64_t *__restrict__ prop, uint32_t m, int64_t
             for (int i = 0; i < na; ++i)
                 if (gid[i] == fn) a = i;
             if (a < 0) {  // a passive miner finds a block: it leaves the class with the class's chain
-                if (na == WA) {
-                    err |= WERR_EP;
+                if (na == CA) {
+                    cap = 1;
                     break;
                 }
                 a = na;
@@ -229,8 +236,8 @@ MSIM_HDN void wide_episode(const int64_t *__restrict__ prop, uint32_t m, int64_t
                 nf[a] = 0;
                 ++na;
             }
-            if (nb == WE) {
-                err |= WERR_EP;
+            if (nb == CE) {
+                cap = 1;
                 break;
             }
             par[nb] = tip[a];  // Miner::FoundBlock, honest (simulation.h:73-75)
@@ -252,7 +259,7 @@ MSIM_HDN void wide_episode(const int64_t *__restrict__ prop, uint32_t m, int64_t
                 fn = f;
             }
         }
-        if (err) break;
+        if (err || cap) break;
         // BestChain(cur) (main.cpp:68-82): candidates in index order; the passive class sits at the lowest
         // index that is not active.
         uint32_t pmin = 0;
@@ -320,6 +327,12 @@ MSIM_HDN void wide_episode(const int64_t *__restrict__ prop, uint32_t m, int64_t
             }
         }
         cur = ea;
+    }
+    if (cap) {
+        o.end = s;
+        o.flags = WREC_RETRY;
+        o.ne = 0;
+        return;
     }
     if (ended && !err) {
         // BestChain(duration_time) (main.cpp:185), no notification.

@@ -58,7 +58,8 @@ __device__ __forceinline__ uint64_t wave_excl_scan(uint64_t x, uint32_t lane)
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 
 struct W1Lds {
-    const uint32_t *cumw, *fthr, *bucket;
+    const uint64_t *cf;
+    const uint16_t *bucket;
     uint32_t *hist;  // this wave's run
     uint32_t *cc;    // this wave's candidate counter
 };
@@ -68,18 +69,19 @@ __device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogEntry
                                uint32_t nblk, uint32_t b0, uint32_t phase, uint32_t lane, uint32_t r, uint32_t &flast,
                                uint32_t &nc, uint32_t &pick_err_blk, uint32_t &err)
 {
-    uint32_t Icur = draw_interval(ri, lt);
-    uint32_t fcur = wide_pick(rng_next(rp), s.cumw, s.bucket, a.m, a.W, a.mult);
+    uint32_t Icur = draw_interval(ri, lt), thcur;
+    uint32_t fcur = wide_pick(rng_next(rp), s.cf, s.bucket, a.W, a.mult, thcur);
     uint64_t tsum = 0;
     nc = 0;
     for (uint32_t b = 0; b < nblk; ++b) {
         const uint32_t Inext = draw_interval(ri, lt);
-        const uint32_t fnext = wide_pick(rng_next(rp), s.cumw, s.bucket, a.m, a.W, a.mult);
+        uint32_t thnext;
+        const uint32_t fnext = wide_pick(rng_next(rp), s.cf, s.bucket, a.W, a.mult, thnext);
         tsum += Icur;
         bool slow = false;
         if (fcur < a.m) {
             atomicAdd(&s.hist[fcur], 1u);
-            slow = Inext <= s.fthr[fcur];
+            slow = Inext <= thcur;
         } else if (pick_err_blk == WIDE_NONE) {
             pick_err_blk = b0 + b;
         }
@@ -105,6 +107,7 @@ __device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogEntry
         flast = fcur;
         Icur = Inext;
         fcur = fnext;
+        thcur = thnext;
     }
     return tsum;
 }
@@ -114,15 +117,14 @@ __device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogEntry
 // ---------------------------------------------------------------- W1
 __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
 {
-    extern __shared__ uint32_t sh[];
+    extern __shared__ uint64_t sh64[];
     __shared__ LogEntry s_log[LOG_TAB];
     __shared__ uint32_t s_cc[4];
     const uint32_t m = a.m, tid = threadIdx.x;
-    uint32_t *s_cumw = sh, *s_fthr = sh + m, *s_bkt = sh + 2 * m, *s_hist = sh + 2 * m + WB_N;
-    for (uint32_t i = tid; i < m; i += 256) {
-        s_cumw[i] = a.cumw[i];
-        s_fthr[i] = a.fthr[i];
-    }
+    uint64_t *s_cf = sh64;                                    // [m + 1]
+    uint16_t *s_bkt = (uint16_t *)(sh64 + m + 1);             // [WB_N]
+    uint32_t *s_hist = (uint32_t *)(s_bkt + WB_N);            // [4][m]
+    for (uint32_t i = tid; i <= m; i += 256) s_cf[i] = a.cf[i];
     for (uint32_t i = tid; i < WB_N; i += 256) s_bkt[i] = a.bucket[i];
     for (uint32_t i = tid; i < 4 * m; i += 256) s_hist[i] = 0;
     for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = a.logt[i];
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
     const uint32_t w = tid >> 6, lane = tid & 63u;
     const uint32_t r = blockIdx.x * 4 + w;  // slice-local run
     if (r >= a.n) return;                   // wave-uniform; no block barrier below
-    const W1Lds s{s_cumw, s_fthr, s_bkt, s_hist + w * m, s_cc + w};
+    const W1Lds s{s_cf, s_bkt, s_hist + w * m, s_cc + w};
     const uint64_t run = a.run_begin + r;
     const Rng ri0 = rng_seed(seed_interval(a.seed_base, run));
     const Rng rp0 = rng_seed(seed_picker(a.seed_base, run));
@@ -166,7 +168,8 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
             if (lane > Ls) {  // every block of the segment is past the end: take them out again
                 Rng p = rps;
                 for (uint32_t b = 0; b < nblk; ++b) {
-                    const uint32_t f = wide_pick(rng_next(p), s.cumw, s.bucket, m, a.W, a.mult);
+                    uint32_t th;
+                    const uint32_t f = wide_pick(rng_next(p), s.cf, s.bucket, a.W, a.mult, th);
                     if (f < m) atomicSub(&s.hist[f], 1u);
                 }
             } else if (lane == Ls) {
@@ -176,7 +179,8 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
                 tl = t0;
                 for (uint32_t b = 0; b < nblk; ++b) {
                     T += (uint32_t)draw_interval(i2, s_log);
-                    const uint32_t f = wide_pick(rng_next(p2), s.cumw, s.bucket, m, a.W, a.mult);
+                    uint32_t th;
+                    const uint32_t f = wide_pick(rng_next(p2), s.cf, s.bucket, a.W, a.mult, th);
                     if ((int64_t)T >= D) {
                         if (ne == WIDE_NONE) ne = b0 + b;
                         if (f < m) atomicSub(&s.hist[f], 1u);
@@ -240,6 +244,9 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
 }
 
 // ---------------------------------------------------------------- W2
+// RETRY = false: every candidate with small capacities (WE_FAST, WA_FAST); RETRY = true: only the
+// candidates the first pass flagged WREC_RETRY, with the record format's full capacities.
+template <bool RETRY>
 __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a)
 {
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -247,8 +254,9 @@ __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a
     if (r >= a.n) return;
     const uint32_t *inf = a.info + (size_t)r * 4;
     if (c >= inf[2]) return;
-    const WideCand e = a.cand[idx];
     uint32_t *rec = a.recs + idx * WREC_WORDS;
+    if (RETRY && !(rec[1] & WREC_RETRY)) return;
+    const WideCand e = a.cand[idx];
     if (inf[3] != 0 || e.block >= inf[0]) {  // failed run, or a block past the end of the run
         rec[0] = e.block + 1;
         rec[1] = WREC_SKIP;
@@ -257,9 +265,14 @@ __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a
     }
     const WideLane ln = a.lanes[((size_t)r * (1 + a.nch) + e.phase) * 64 + (e.lane_seq >> 16)];
     const int64_t Ts = (int64_t)(ln.t0 + e.offset);
-    WideSrc src{e.ri, e.rp, a.logt, a.cumw, a.bucket, a.m, a.W, a.mult};
+    WideSrc src{e.ri, e.rp, a.logt, a.cf, a.bucket, a.W, a.mult};
     WideEpOut o;
-    wide_episode(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
+    if (RETRY) {
+        wide_episode<WE, WA>(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
+        if (o.flags & WREC_RETRY) o.flags = WREC_ERR;
+    } else {
+        wide_episode<WE_FAST, WA_FAST>(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
+    }
     rec[0] = o.end;
     rec[1] = o.flags;
     rec[2] = o.ne;
@@ -318,7 +331,8 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             }
         }
         wave_sync();
-        // chain the episodes whose first block is reached quiet (serial over the sorted list)
+        // chain the episodes whose first block is reached quiet: a serial walk over the sorted list in
+        // LDS marks them (bit 15 of the slot field), then all lanes apply the marked episodes' deltas
         uint32_t cursor = 0;
         bool run_ended = false;
         if (ok) {
@@ -326,19 +340,12 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
                 const uint32_t sblk = KB[i];
                 if (sblk >= n_end) break;
                 if (sblk < cursor) continue;
-                const uint32_t fl = KF[i] >> 16, c = KF[i] & 0xFFFFu;
-                if (fl & (WREC_ERR | WREC_SKIP)) {
+                const uint32_t kf = KF[i], fl = kf >> 16;
+                if (fl & (WREC_ERR | WREC_SKIP | WREC_RETRY)) {
                     ok = false;
                     break;
                 }
-                const uint32_t *rec = a.recs + ((size_t)r * a.rcap + c) * WREC_WORDS;
-                const uint32_t ne = rec[2];
-                if (lane < ne) {
-                    const uint32_t g = rec[4 + 3 * lane];
-                    F[g] += rec[5 + 3 * lane];
-                    S[g] += rec[6 + 3 * lane];
-                }
-                wave_sync();
+                if (lane == 0) KF[i] = kf | 0x8000u;
                 cursor = KE[i];
                 if (fl & WREC_ENDED) {
                     run_ended = true;
@@ -346,6 +353,21 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
                 }
             }
         }
+        wave_sync();
+        if (ok) {
+            for (uint32_t i = lane; i < cc; i += 64) {
+                const uint32_t kf = KF[i];
+                if (!(kf & 0x8000u)) continue;
+                const uint32_t *rec = a.recs + ((size_t)r * a.rcap + (kf & 0x7FFFu)) * WREC_WORDS;
+                const uint32_t ne = rec[2];
+                for (uint32_t j = 0; j < ne; ++j) {
+                    const uint32_t g = rec[4 + 3 * j];
+                    atomicAdd(&F[g], rec[5 + 3 * j]);
+                    atomicAdd(&S[g], rec[6 + 3 * j]);
+                }
+            }
+        }
+        wave_sync();
         // the run ended quiet and its last block was fast: it counts only if it arrived by D (main.cpp:185)
         if (ok && lane == 0 && !run_ended && n_end > 0 && cursor < n_end && lastf < m) {
             if (a.tlast[r] + a.prop[lastf] > D) F[lastf] -= 1u;
@@ -400,18 +422,19 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
 }
 
 // ---------------------------------------------------------------- weighted pick (test surface)
-__global__ void msim_wide_pick_kernel(const uint32_t *__restrict__ cumw, const uint32_t *__restrict__ bucket, uint32_t m,
+__global__ void msim_wide_pick_kernel(const uint64_t *__restrict__ cf, const uint16_t *__restrict__ bucket, uint32_t m,
                                       uint32_t W, uint64_t mult, const uint64_t *__restrict__ u, int32_t *__restrict__ out,
                                       uint64_t n)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t k = wide_pick(u[i], cumw, bucket, m, W, mult);
+    uint32_t th;
+    const uint32_t k = wide_pick(u[i], cf, bucket, W, mult, th);
     out[i] = k >= m ? -1 : (int32_t)k;
 }
 
 // ---------------------------------------------------------------- host side
-size_t wide_w1_lds(uint32_t m) { return ((size_t)2 * m + WB_N + 4 * (size_t)m) * 4; }
+size_t wide_w1_lds(uint32_t m) { return ((size_t)m + 1) * 8 + (size_t)WB_N * 2 + 4 * (size_t)m * 4; }
 size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch)
 {
     return (size_t)4 * m * 8 + 4 * ((size_t)2 * m + 3 * (size_t)rcap + (size_t)(1 + nch) * 64) * 4;
@@ -450,7 +473,9 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
         hipLaunchKernelGGL(msim_wide_draws_kernel, dim3((cn + 3) / 4), dim3(256), l1, s, a);
         if (ee) (void)hipEventRecord(ee, s);
         const size_t nthreads = (size_t)cn * a.rcap;
-        hipLaunchKernelGGL(msim_wide_episode_kernel, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, s, a);
+        const dim3 g2((unsigned)((nthreads + 255) / 256));
+        hipLaunchKernelGGL(msim_wide_episode_kernel<false>, g2, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(msim_wide_episode_kernel<true>, g2, dim3(256), 0, s, a);
         WideOut o = out;
         o.rel_begin = (uint32_t)off;
         uint32_t g3 = (cn + 3) / 4;
@@ -465,7 +490,7 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
 hipError_t launch_wide_picks(const WideArgs &a, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(msim_wide_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.cumw, a.bucket, a.m,
+    hipLaunchKernelGGL(msim_wide_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.cf, a.bucket, a.m,
                        a.W, a.mult, u, out, n);
     return hipGetLastError();
 }

@@ -11,7 +11,8 @@ namespace msim {
 
 struct WideArgs {
     // per-config device tables
-    const uint32_t *cumw, *bucket, *fthr;  // [m], [WB_N], [m] (fast threshold = prop clamped to FTHR_NEVER)
+    const uint64_t *cf;       // [m + 1] cumulative weight | fast threshold << 32 (msim_wide.h wide_pick)
+    const uint16_t *bucket;   // [WB_N]
     const int64_t *prop;                   // [m] propagation (ms)
     const LogEntry *logt;
     const uint32_t *jmain;  // [64][128] uint4: T^(lane * S0)
@@ -59,7 +60,7 @@ inline WideLayout wide_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     const double blocks = (double)L.g.B0 + 64.0 * L.g.ST * L.g.nch + 64.0;
     const double lam = rho * blocks;
     double rc = ceil(lam + 8.0 * sqrt(lam) + 16.0);
-    if (rc > 60000.0) rc = 60000.0;
+    if (rc > 32000.0) rc = 32000.0;  // slot index fits 15 bits in the combine
     L.rcap = (uint32_t)rc;
     const double per_run = m * 4.0 + 16 + 8 + (1.0 + L.g.nch) * 64 * sizeof(WideLane) +
                            L.rcap * (sizeof(WideCand) + 4.0 * WREC_WORDS) + 64;

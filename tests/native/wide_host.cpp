@@ -16,11 +16,14 @@ using namespace msim;
 
 extern "C" int wide_host_pick(const uint64_t *w, uint32_t m, uint64_t W, const uint64_t *u, int32_t *out, uint64_t n)
 {
-    std::vector<uint32_t> cumw(m), bucket(WB_N);
-    build_wide_pick(w, m, (uint32_t)W, cumw.data(), bucket.data());
+    std::vector<uint64_t> cf(m + 1);
+    std::vector<uint16_t> bucket(WB_N);
+    std::vector<uint32_t> fthr(m, 0);
+    build_wide_pick(w, fthr.data(), m, (uint32_t)W, cf.data(), bucket.data());
     const uint64_t mult = 0xFFFFFFFFFFFFFFFFull / W;
     for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t k = wide_pick(u[i], cumw.data(), bucket.data(), m, (uint32_t)W, mult);
+        uint32_t th;
+        const uint32_t k = wide_pick(u[i], cf.data(), bucket.data(), (uint32_t)W, mult, th);
         out[i] = k >= m ? -1 : (int32_t)k;
     }
     return 0;
@@ -31,13 +34,15 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
                              uint32_t seed_base, uint64_t run_begin, uint32_t n, uint32_t *found, uint32_t *stale,
                              uint32_t *err_out, uint32_t *n_episodes)
 {
-    std::vector<uint32_t> cumw(m), bucket(WB_N), fthr(m);
-    build_wide_pick(w, m, (uint32_t)W, cumw.data(), bucket.data());
+    std::vector<uint64_t> cf(m + 1);
+    std::vector<uint16_t> bucket(WB_N);
+    std::vector<uint32_t> fthr(m);
     for (uint32_t k = 0; k < m; ++k) fthr[k] = prop[k] < (int64_t)FTHR_NEVER ? (uint32_t)prop[k] : FTHR_NEVER;
+    build_wide_pick(w, fthr.data(), m, (uint32_t)W, cf.data(), bucket.data());
     std::vector<LogEntry> lt(LOG_TAB);
     build_log_table(lt.data());
     const uint64_t mult = 0xFFFFFFFFFFFFFFFFull / W;
-    uint32_t neps = 0;
+    uint32_t neps = 0, n_retry = 0;
     for (uint32_t r = 0; r < n; ++r) {
         const uint64_t run = run_begin + r;
         Rng ri = rng_seed(seed_interval(seed_base, run)), rp = rng_seed(seed_picker(seed_base, run));
@@ -48,7 +53,8 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
         // draw until the first block at >= D, plus one more (its successor decides fast/slow)
         for (;;) {
             const uint32_t x = draw_interval(ri, lt.data());
-            const uint32_t f = wide_pick(rng_next(rp), cumw.data(), bucket.data(), m, (uint32_t)W, mult);
+            uint32_t th;
+            const uint32_t f = wide_pick(rng_next(rp), cf.data(), bucket.data(), (uint32_t)W, mult, th);
             t += x;
             I.push_back(x);
             F.push_back(f);
@@ -72,9 +78,14 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
         for (uint32_t s = 0; s < n_end && !err; ++s) {
             if (s < cursor) continue;
             if (!(I[s + 1] <= fthr[F[s]])) continue;  // fast block
-            WideSrc src{SI[s + 1], SP[s + 1], lt.data(), cumw.data(), bucket.data(), m, (uint32_t)W, mult};
+            WideSrc src{SI[s + 1], SP[s + 1], lt.data(), cf.data(), bucket.data(), (uint32_t)W, mult};
             WideEpOut o;
-            wide_episode(prop, m, D, s, T[s], F[s], I[s + 1], F[s + 1], src, o);
+            wide_episode<WE_FAST, WA_FAST>(prop, m, D, s, T[s], F[s], I[s + 1], F[s + 1], src, o);
+            if (o.flags & WREC_RETRY) {  // the device's retry pass: same episode, larger capacities
+                WideSrc src2{SI[s + 1], SP[s + 1], lt.data(), cf.data(), bucket.data(), (uint32_t)W, mult};
+                wide_episode<WE, WA>(prop, m, D, s, T[s], F[s], I[s + 1], F[s + 1], src2, o);
+                ++n_retry;
+            }
             ++neps;
             if (o.flags & WREC_ERR) {
                 err |= WERR_EP;
@@ -96,6 +107,6 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
         }
         err_out[r] = err;
     }
-    if (n_episodes) *n_episodes = neps;
+    if (n_episodes) *n_episodes = neps | (n_retry << 24);
     return 0;
 }

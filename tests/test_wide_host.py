@@ -57,13 +57,13 @@ def test_default_network_year(wide, oracle, prop):
     """W = 100: the same networks the narrow path runs, through the large-network engine."""
     _, s, neps = _check(wide, oracle, H9, [prop] * 9, 100, YEAR, 8)
     if prop >= 1000:
-        assert neps > 0 and s.sum() > 0
+        assert neps & 0xFFFFFF > 0 and s.sum() > 0
 
 
 def test_c5_network_month(wide, oracle):
     w, p, W = c5_network()
     f, s, neps = _check(wide, oracle, w, p, W, 30 * DAY, 6)
-    assert neps > 0
+    assert neps & 0xFFFFFF > 0
 
 
 def test_c5_network_year(wide, oracle):
@@ -82,6 +82,14 @@ def test_random_weighted_networks(wide, oracle, seed):
     W = sum(w)
     props = [rnd.choice([0, 1, 50, 700, 3000, 20_000]) for _ in range(m)]
     _check(wide, oracle, w, props, W, rnd.choice([DAY, 20 * DAY, 90 * DAY]), 6, base=rnd.randrange(1 << 32))
+
+
+def test_retry_capacities_exercised(wide, oracle):
+    """Long propagation (30 s) forks often enough that some episodes outgrow the first pass's capacities
+    (WE_FAST blocks / WA_FAST miners) and take the retry instantiation; results stay exact."""
+    w = [5] * 20
+    _, _, neps = _check(wide, oracle, w, [30_000] * 20, 100, YEAR, 8)
+    assert neps >> 24 > 0, "no episode needed the retry capacities"
 
 
 @pytest.mark.parametrize("duration", [0, 1, 599_999, 600_000, 3 * DAY])
@@ -105,7 +113,7 @@ def test_weighted_pick_matches_oracle(native_tests, oracle):
                 x = int(c) * mult + d
                 if 0 <= x < 1 << 64:
                     edges.append(x)
-        edges += [(b << 54) + d for b in range(1024) for d in (0, 1) if (b << 54) + d < (1 << 64)] + [(1 << 64) - 1]
+        edges += [(b << 52) + d for b in range(4096) for d in (-1, 0, 1) if 0 <= (b << 52) + d < (1 << 64)] + [(1 << 64) - 1]
         uu = np.concatenate([u, np.array(edges, dtype=np.uint64)])
         out = (ctypes.c_int32 * len(uu))()
         lib.wide_host_pick((ctypes.c_uint64 * len(weights))(*weights), ctypes.c_uint32(len(weights)), ctypes.c_uint64(W),
