@@ -67,7 +67,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5", "default"])
-    ap.add_argument("--runs", type=int, default=0, help="runs per GPU per step (0: 32768; c5: 65536)")
+    ap.add_argument("--runs", type=int, default=0,
+                    help="runs per GPU per step (0: 32768 = SIM_RUNS; c3: 131072 = configs[2]'s 1M runs / 8 GPUs; c5: 65536)")
     ap.add_argument("--seed-base", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
@@ -90,7 +91,7 @@ def main() -> None:
     miners = PRESETS[args.config]()
     m = len(miners)
     sim = Simulation(miners, total_weight=PRESET_WEIGHTS.get(args.config, 100))
-    n = args.runs or (65536 if args.config == "c5" else 32768)
+    n = args.runs or {"c3": 131072, "c5": 65536}.get(args.config, 32768)
     dev = torch.device("cuda", local)
     ws = torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev)
     sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)

@@ -33,7 +33,7 @@ __device__ __forceinline__ void block_reduce_store(const uint64_t (&v)[6 * M], u
 }
 
 template <int M, bool SELF, bool DEEP, int NX, int NG, bool LIST>
-__global__ __launch_bounds__(TPB) void msim_runs_kernel(const SimParams p, const uint64_t run_begin, const uint32_t n,
+__global__ __launch_bounds__(TPB, 2) void msim_runs_kernel(const SimParams p, const uint64_t run_begin, const uint32_t n,
                                                          const uint32_t seed_base, const uint32_t *__restrict__ list,
                                                          const uint32_t *__restrict__ list_count, const uint32_t list_cap,
                                                          uint64_t *__restrict__ partials, uint32_t *__restrict__ records,
@@ -112,7 +112,7 @@ __device__ __forceinline__ void stats_terms(const RunResult &r, uint64_t (&v)[6 
 // uniform (scalar loads from pts[point]) and its partial sums belong to one point. LIST: the retry
 // pass over flagged lanes (codes point * wpp * TPB + rel), wide capacities, atomic per-point sums.
 template <int M, bool SELF, bool DEEP, int NX, int NG, bool LIST>
-__global__ __launch_bounds__(TPB) void msim_sweep_kernel(const SimParams *__restrict__ pts, const uint64_t run_begin,
+__global__ __launch_bounds__(TPB, 2) void msim_sweep_kernel(const SimParams *__restrict__ pts, const uint64_t run_begin,
                                                           const uint32_t rpp, const uint32_t wpp, const uint32_t seed_base,
                                                           const uint32_t *__restrict__ list, const uint32_t *__restrict__ list_count,
                                                           const uint32_t list_cap, uint64_t *__restrict__ partials,
