@@ -156,6 +156,24 @@ typedef struct msim_pipeline_layout {
 } msim_pipeline_layout;
 int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_layout *out);
 
+/* GPU-scale forms of test.cpp's samplers. One RNG stream RNG{seed} (xoroshiro128++.h:23)
+ * of n draws, exactly as the reference's single loops draw it (integer results identical for any n):
+ *   msim_sample_picks      out_counts[k] = #{i < n : PickFinder(draw i) == k}, k < M; out_counts[M] = draws
+ *                          where PickFinder would assert (simulation.h:220). test.cpp:15-63
+ *                          MinerPickerSample (10^8 picks over 100 miners of 1 %) and the stream of
+ *                          test.cpp:68-118 MinerPickerSmallBig. out_counts: M + 1 host entries.
+ *   msim_sample_intervals  exact integer moments of n NextBlockInterval draws (simulation.h:205-210):
+ *                          test.cpp:191-208 BlockIntervalSample (mean and std dev follow from them).
+ * Synchronous, on HIP device `device`. */
+typedef struct msim_interval_moments {
+    uint64_t n;
+    uint64_t sum;                /* sum of intervals (ms) */
+    uint64_t sumsq_lo, sumsq_hi; /* sum of squared intervals, 128-bit */
+    uint64_t max;                /* largest interval (ms) */
+} msim_interval_moments;
+int msim_sample_picks(const msim_config *cfg, uint64_t seed, uint64_t n, uint64_t *out_counts, int device);
+int msim_sample_intervals(uint64_t seed, uint64_t n, msim_interval_moments *out, int device);
+
 /* Convert fixed-point sums to MinerStats-style doubles. */
 void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out);
 

@@ -8,6 +8,8 @@ from ._lib import MsimError, LIB_PATH  # noqa: F401  (raises ImportError when li
 from .simulation import (  # noqa: F401
     C4_PROPAGATIONS_MS,
     C4_SELFISH_PERCS,
+    C5_TOTAL_WEIGHT,
+    PRESET_WEIGHTS,
     DEFAULT_SEED_BASE,
     PRESETS,
     SIM_DURATION_MS,
@@ -18,12 +20,17 @@ from .simulation import (  # noqa: F401
     SimulationResult,
     Sweep,
     c4_grid,
+    c5_network,
     exact_stats_total,
     report,
+    sample_intervals,
+    sample_picks,
     setup_miners,
     sums_to_stats,
     timing_enable,
     timing_read,
 )
+
+from . import model  # noqa: F401,E402  (first-order analytical stale-rate model, plot.py restated)
 
 __version__ = "0.1.0"

@@ -46,6 +46,8 @@ EXPORTED = (
     "msim_sweep_run",
     "msim_strerror",
     "msim_version",
+    "msim_sample_picks",
+    "msim_sample_intervals",
 )
 
 
@@ -93,6 +95,11 @@ class MsimError(RuntimeError):
     def __init__(self, code: int, what: str = ""):
         self.code = code
         super().__init__(f"{what}: {strerror(code)} ({code})" if what else f"{strerror(code)} ({code})")
+
+
+class MsimIntervalMoments(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("sum", ctypes.c_uint64), ("sumsq_lo", ctypes.c_uint64),
+                ("sumsq_hi", ctypes.c_uint64), ("max", ctypes.c_uint64)]
 
 
 def _load() -> ctypes.CDLL:
@@ -148,6 +155,10 @@ def _load() -> ctypes.CDLL:
     lib.msim_sweep_run.restype = ctypes.c_int
     lib.msim_strerror.argtypes = [ctypes.c_int]
     lib.msim_strerror.restype = ctypes.c_char_p
+    lib.msim_sample_picks.argtypes = [vp, u64, u64, ctypes.POINTER(u64), ctypes.c_int]
+    lib.msim_sample_picks.restype = ctypes.c_int
+    lib.msim_sample_intervals.argtypes = [u64, u64, ctypes.POINTER(MsimIntervalMoments), ctypes.c_int]
+    lib.msim_sample_intervals.restype = ctypes.c_int
     lib.msim_version.argtypes = []
     lib.msim_version.restype = ctypes.c_char_p
     return lib

@@ -799,6 +799,92 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     return MSIM_OK;
 }
 
+// ---------------------------------------------------------------- samplers (test.cpp)
+namespace {
+int sample_impl(int mode, const msim_config *cfg, uint64_t seed, uint64_t n, int device, unsigned long long *host_out,
+                size_t nout)
+{
+    using namespace msim;
+    if (hipSetDevice(device) != hipSuccess) return MSIM_E_HIP;
+    const uint64_t target_threads = 131072;
+    uint64_t S64 = (n + target_threads - 1) / target_threads;
+    if (S64 < 64) S64 = 64;
+    if (S64 > 0xFFFFFFFFull) return MSIM_E_INVALID;
+    const uint32_t S = (uint32_t)S64;
+    // T^(S * 2^b), b = 0..31
+    std::vector<uint32_t> jumps(32 * 512);
+    {
+        Mat128 cur, tmp;
+        mat_pow(S, cur);
+        for (int b = 0; b < 32; ++b) {
+            uint32_t *w = jumps.data() + (size_t)b * 512;
+            for (int col = 0; col < 128; ++col) {
+                w[4 * col + 0] = (uint32_t)cur.lo[col];
+                w[4 * col + 1] = (uint32_t)(cur.lo[col] >> 32);
+                w[4 * col + 2] = (uint32_t)cur.hi[col];
+                w[4 * col + 3] = (uint32_t)(cur.hi[col] >> 32);
+            }
+            mat_mul(cur, cur, tmp);
+            cur = tmp;
+        }
+    }
+    uint32_t m = 0, W = 100;
+    std::vector<uint64_t> cf(1, 0xFFFFFFFFull);
+    std::vector<uint16_t> bucket(WB_N, 0);
+    if (mode == 0) {
+        m = cfg->n;
+        W = (uint32_t)cfg->total_weight;
+        std::vector<uint64_t> w(m);
+        for (uint32_t k = 0; k < m; ++k) w[k] = cfg->wide ? cfg->wperc[k] : cfg->perc[k];
+        std::vector<uint32_t> fthr(m, 0);
+        cf.assign(m + 1, 0);
+        build_wide_pick(w.data(), fthr.data(), m, W, cf.data(), bucket.data());
+    }
+    LogEntry lt[LOG_TAB];
+    build_log_table(lt);
+    const size_t bj = jumps.size() * 4, bc = cf.size() * 8, bb = bucket.size() * 2, bl = sizeof(lt), bo = nout * 8;
+    char *d = nullptr;
+    int rc = MSIM_OK;
+    hipStream_t st = nullptr;
+    if (hipMalloc((void **)&d, bj + bc + bb + bl + bo + 64) != hipSuccess || hipStreamCreate(&st) != hipSuccess) {
+        (void)hipFree(d);
+        return MSIM_E_HIP;
+    }
+    char *pj = d, *pc = pj + bj, *pb = pc + bc, *pl = pb + ((bb + 7) / 8 * 8), *po = pl + bl;
+    if (hipMemcpyAsync(pj, jumps.data(), bj, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(pc, cf.data(), bc, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(pb, bucket.data(), bb, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(pl, lt, bl, hipMemcpyHostToDevice, st) != hipSuccess || hipMemsetAsync(po, 0, bo, st) != hipSuccess ||
+        launch_sample(mode, (const uint32_t *)pj, seed, n, S, (const uint64_t *)pc, (const uint16_t *)pb, m, W,
+                      0xFFFFFFFFFFFFFFFFull / W, (const LogEntry *)pl, (unsigned long long *)po, st) != hipSuccess ||
+        hipMemcpyAsync(host_out, po, bo, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+        rc = MSIM_E_HIP;
+    (void)hipStreamDestroy(st);
+    (void)hipFree(d);
+    return rc;
+}
+}  // namespace
+
+int msim_sample_picks(const msim_config *cfg, uint64_t seed, uint64_t n, uint64_t *out_counts, int device)
+{
+    if (!cfg || !out_counts) return MSIM_E_INVALID;
+    return sample_impl(0, cfg, seed, n, device, (unsigned long long *)out_counts, cfg->n + 1);
+}
+
+int msim_sample_intervals(uint64_t seed, uint64_t n, msim_interval_moments *out, int device)
+{
+    if (!out) return MSIM_E_INVALID;
+    unsigned long long o[4] = {0, 0, 0, 0};
+    const int rc = sample_impl(1, nullptr, seed, n, device, o, 4);
+    if (rc) return rc;
+    out->n = n;
+    out->sum = o[0];
+    out->sumsq_lo = o[1];
+    out->sumsq_hi = o[2];
+    out->max = o[3];
+    return MSIM_OK;
+}
+
 const char *msim_strerror(int code)
 {
     switch (code) {

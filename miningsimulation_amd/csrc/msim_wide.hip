@@ -496,3 +496,103 @@ hipError_t launch_wide_picks(const WideArgs &a, const uint64_t *u, int32_t *out,
 }
 
 }  // namespace msim
+
+// ---------------------------------------------------------------- samplers (test.cpp)
+// One RNG stream of n draws (test.cpp's MinerPickerSample / BlockIntervalSample loops) split into
+// segments of S draws, one per thread: thread j jumps to draw j*S with the wave-uniform matrices
+// T^(S*2^b) applied where bit b of j is set, then draws its segment sequentially — the same draws the
+// reference's single loop makes, so the integer results are identical to it for any n.
+namespace msim {
+namespace {
+
+__device__ __forceinline__ void jump_masked(const uint4 *__restrict__ cols, Rng &a, bool apply)
+{
+    const uint32_t sa[4] = {(uint32_t)a.s0, (uint32_t)(a.s0 >> 32), (uint32_t)a.s1, (uint32_t)(a.s1 >> 32)};
+    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll 8
+        for (int i = 0; i < 32; ++i) {
+            const uint4 c = cols[w * 32 + i];
+            const uint32_t mk = 0u - ((sa[w] >> i) & 1u);
+            o0 ^= c.x & mk;
+            o1 ^= c.y & mk;
+            o2 ^= c.z & mk;
+            o3 ^= c.w & mk;
+        }
+    }
+    if (apply) {
+        a.s0 = (uint64_t)o0 | ((uint64_t)o1 << 32);
+        a.s1 = (uint64_t)o2 | ((uint64_t)o3 << 32);
+    }
+}
+
+}  // namespace
+
+// MODE 0: pick counts ([m + 1] bins, bin m = fell through); MODE 1: interval moments
+// (out[0] = sum, out[1] = sum of squares lo, out[2] = hi, out[3] = max).
+template <int MODE>
+__global__ __launch_bounds__(256) void msim_sample_kernel(const uint32_t *__restrict__ pow2_jumps, uint64_t seed,
+                                                           uint64_t n, uint32_t S, const uint64_t *__restrict__ cf,
+                                                           const uint16_t *__restrict__ bucket, uint32_t m, uint32_t W,
+                                                           uint64_t mult, const LogEntry *__restrict__ logt,
+                                                           unsigned long long *__restrict__ out)
+{
+    extern __shared__ uint32_t s_hist[];  // MODE 0: [m + 1]
+    __shared__ LogEntry s_log[LOG_TAB];
+    const uint32_t tid = threadIdx.x;
+    if (MODE == 0)
+        for (uint32_t i = tid; i <= m; i += 256) s_hist[i] = 0;
+    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = logt[i];
+    __syncthreads();
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + tid;
+    const uint64_t b0 = j * S;
+    const uint32_t cnt = b0 < n ? (uint32_t)((n - b0) < S ? (n - b0) : S) : 0u;
+    Rng r = rng_seed(seed);
+    for (int b = 0; b < 32 && ((uint64_t)gridDim.x * 256 >> b) > 0; ++b) {
+        const bool bit = (j >> b) & 1u;
+        if (__ballot(bit)) jump_masked(reinterpret_cast<const uint4 *>(pow2_jumps) + (size_t)b * 128, r, bit);
+    }
+    uint64_t sum = 0, sq = 0, mx = 0;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        if (MODE == 0) {
+            uint32_t th;
+            const uint32_t k = wide_pick(rng_next(r), cf, bucket, W, mult, th);
+            atomicAdd(&s_hist[k < m ? k : m], 1u);
+        } else {
+            const uint64_t x = (uint64_t)draw_interval(r, s_log);
+            sum += x;
+            sq += x * x;
+            mx = x > mx ? x : mx;
+        }
+    }
+    if (MODE == 0) {
+        __syncthreads();
+        for (uint32_t i = tid; i <= m; i += 256)
+            if (s_hist[i]) atomicAdd(&out[i], (unsigned long long)s_hist[i]);
+    } else if (cnt) {
+        atomicAdd(&out[0], (unsigned long long)sum);
+        const unsigned long long old = atomicAdd(&out[1], (unsigned long long)sq);
+        if (old + sq < old) atomicAdd(&out[2], 1ull);  // carry into the high word
+        atomicMax(&out[3], (unsigned long long)mx);
+    }
+}
+
+// pow2_jumps: 32 matrices T^(S * 2^b) (msim_jump.h layout) in device memory.
+hipError_t launch_sample(int mode, const uint32_t *pow2_jumps, uint64_t seed, uint64_t n, uint32_t S, const uint64_t *cf,
+                         const uint16_t *bucket, uint32_t m, uint32_t W, uint64_t mult, const LogEntry *logt,
+                         unsigned long long *out, hipStream_t s)
+{
+    const uint64_t threads = (n + S - 1) / S;
+    const uint32_t grid = (uint32_t)((threads + 255) / 256);
+    if (grid == 0) return hipSuccess;
+    if (mode == 0)
+        hipLaunchKernelGGL(msim_sample_kernel<0>, dim3(grid), dim3(256), (m + 1) * 4, s, pow2_jumps, seed, n, S, cf, bucket,
+                           m, W, mult, logt, out);
+    else
+        hipLaunchKernelGGL(msim_sample_kernel<1>, dim3(grid), dim3(256), 0, s, pow2_jumps, seed, n, S, cf, bucket, m, W,
+                           mult, logt, out);
+    return hipGetLastError();
+}
+
+}  // namespace msim

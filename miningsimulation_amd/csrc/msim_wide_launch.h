@@ -90,6 +90,9 @@ size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch);
 // Runs out.n_total runs slice by slice (L.nr) on stream s; proto carries the tables and geometry.
 hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, const WideOut &out, hipStream_t s,
                        std::vector<hipEvent_t> *w1_events);
+hipError_t launch_sample(int mode, const uint32_t *pow2_jumps, uint64_t seed, uint64_t n, uint32_t S, const uint64_t *cf,
+                         const uint16_t *bucket, uint32_t m, uint32_t W, uint64_t mult, const LogEntry *logt,
+                         unsigned long long *out, hipStream_t s);
 hipError_t launch_wide_picks(const WideArgs &a, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
 
 }  // namespace msim

@@ -188,6 +188,27 @@ class Simulation:
               "msim_launch")
 
 
+def sample_picks(sim: "Simulation", seed: int, n: int, device: int = 0) -> np.ndarray:
+    """test.cpp:15-63 MinerPickerSample on the GPU: per-miner counts of n PickFinder draws of RNG{seed}
+    (the last entry counts draws where the reference would assert), identical to the sequential loop."""
+    m = len(sim.miners)
+    out = (ctypes.c_uint64 * (m + 1))()
+    check(lib.msim_sample_picks(sim.handle, seed, n, out, device), "msim_sample_picks")
+    return np.array(out[:], dtype=np.uint64)
+
+
+def sample_intervals(seed: int, n: int, device: int = 0) -> dict:
+    """test.cpp:191-208 BlockIntervalSample on the GPU: exact integer moments of n NextBlockInterval draws
+    of RNG{seed}, plus the mean and standard deviation the reference prints."""
+    mo = _lib.MsimIntervalMoments()
+    check(lib.msim_sample_intervals(seed, n, ctypes.byref(mo), device), "msim_sample_intervals")
+    sumsq = (int(mo.sumsq_hi) << 64) | int(mo.sumsq_lo)
+    mean = mo.sum / n if n else 0.0
+    var = sumsq / n - mean * mean if n else 0.0
+    return {"n": int(mo.n), "sum": int(mo.sum), "sumsq": sumsq, "max": int(mo.max), "mean": mean,
+            "std": var ** 0.5 if var > 0 else 0.0}
+
+
 class Sweep:
     """A grid of networks run in ONE device launch (BASELINE configs[3]; msim_sweep_* in include/msim.h).
 

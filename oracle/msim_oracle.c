@@ -515,3 +515,40 @@ void oracle_interval_of_array(const uint64_t *u, int64_t *out, size_t n)
         out[i] = (int64_t)(ns / 1000000LL);
     }
 }
+
+/* ---------------------------------------------------------------- test.cpp samplers (sequential) */
+
+/* test.cpp:15-63 MinerPickerSample: per-miner counts of n PickFinder draws of RNG{seed}; out[n_miners] =
+ * draws that fall through (simulation.h:220 would assert). Weights sum to total_weight (100: percentages). */
+void oracle_pick_counts_w(const uint64_t *perc, int n_miners, uint64_t total_weight, uint64_t seed, uint64_t n,
+                          uint64_t *out)
+{
+    oracle_rng r;
+    oracle_rng_seed(&r, seed);
+    const uint64_t mult = UINT64_MAX / total_weight;
+    for (int k = 0; k <= n_miners; ++k) out[k] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int k = oracle_pick_finder_w(perc, n_miners, mult, &r);
+        out[k < 0 ? n_miners : k]++;
+    }
+}
+
+/* test.cpp:191-208 BlockIntervalSample: exact integer moments of n NextBlockInterval draws of RNG{seed}:
+ * out = {sum, sum of squares (low 64 bits), (high 64 bits), max}. */
+void oracle_interval_moments(uint64_t seed, uint64_t n, uint64_t *out)
+{
+    oracle_rng r;
+    oracle_rng_seed(&r, seed);
+    unsigned __int128 sq = 0;
+    uint64_t sum = 0, mx = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t x = (uint64_t)oracle_next_block_interval(&r);
+        sum += x;
+        sq += (unsigned __int128)x * x;
+        if (x > mx) mx = x;
+    }
+    out[0] = sum;
+    out[1] = (uint64_t)sq;
+    out[2] = (uint64_t)(sq >> 64);
+    out[3] = mx;
+}

@@ -68,6 +68,9 @@ int oracle_state_stale(const oracle_miner_state *s);
 void oracle_state_found_block(oracle_miner_state *s, int64_t block_time, size_t best_chain_size);
 void oracle_state_notify(oracle_miner_state *s, const uint32_t *ids, const int64_t *arrivals, size_t len, int64_t t);
 int64_t oracle_selfish_arrival(void);
+void oracle_pick_counts_w(const uint64_t *perc, int n_miners, uint64_t total_weight, uint64_t seed, uint64_t n,
+                          uint64_t *out);
+void oracle_interval_moments(uint64_t seed, uint64_t n, uint64_t *out);
 void oracle_log1p_array(const double *x, double *out, size_t n);
 void oracle_interval_of_array(const uint64_t *u, int64_t *out, size_t n);
 uint32_t oracle_genesis_id(void);

@@ -62,6 +62,9 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ORunStats), ctypes.POINTER(OSum)]
         L.oracle_pick_finder_w.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_uint64,
                                            ctypes.POINTER(ORng)]
+        L.oracle_pick_counts_w.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_uint64,
+                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_interval_moments.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_rng_seed.argtypes = [ctypes.POINTER(ORng), ctypes.c_uint64]
         L.oracle_rng_rand64.argtypes = [ctypes.POINTER(ORng)]
         L.oracle_rng_rand64.restype = ctypes.c_uint64
@@ -151,6 +154,21 @@ def picks_w(weights: Sequence[int], total_weight: int, seed: int, n: int) -> Lis
     P = (ctypes.c_uint64 * len(weights))(*weights)
     mult = 0xFFFFFFFFFFFFFFFF // total_weight
     return [lib().oracle_pick_finder_w(P, len(weights), mult, ctypes.byref(r)) for _ in range(n)]
+
+
+def pick_counts(weights: Sequence[int], total_weight: int, seed: int, n: int) -> np.ndarray:
+    """test.cpp:15-63 MinerPickerSample, sequential: counts per miner (+ fall-throughs last)."""
+    m = len(weights)
+    out = (ctypes.c_uint64 * (m + 1))()
+    lib().oracle_pick_counts_w((ctypes.c_uint64 * m)(*weights), m, total_weight, seed, n, out)
+    return np.array(out[:], dtype=np.uint64)
+
+
+def interval_moments(seed: int, n: int) -> dict:
+    """test.cpp:191-208 BlockIntervalSample, sequential: exact integer moments."""
+    out = (ctypes.c_uint64 * 4)()
+    lib().oracle_interval_moments(seed, n, out)
+    return {"sum": int(out[0]), "sumsq": (int(out[2]) << 64) | int(out[1]), "max": int(out[3])}
 
 
 def log1p_array(x: np.ndarray) -> np.ndarray:
