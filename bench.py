@@ -29,6 +29,12 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL = 52594.92
 
 
+# HBM bytes per launch of the dominant kernel at the default run counts, from rocprofv3 PMC passes
+# (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, separate passes; profiles/r01/pmc_f1.md).
+# PMC counters cannot be collected inside this process; these are the recorded values of the same command.
+TRAFFIC_PMC = {("c2", 32768): 7.363e9, ("c5", 65536): 9.128e8}
+
+
 def w_blk(m: int) -> int:
     """SURVEY §8(d) fixed accounting convention: algorithmic VALU lane-ops per simulated block."""
     import math
@@ -176,7 +182,10 @@ def main() -> None:
                 "peak": round(VALU_PEAK_LANE_OPS / 1e12, 2),
                 "unit": "T lane-op/s",
                 "frac": round(achieved / VALU_PEAK_LANE_OPS, 5),
-                "traffic": None,
+                "traffic": TRAFFIC_PMC.get((args.config, n)),
+                "traffic_source": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this command, recorded in "
+                                   "profiles/r01/pmc_f1.md (bytes per launch of the draw kernel)")
+                if (args.config, n) in TRAFFIC_PMC else None,
                 "kernel": ("msim_launch = W1 msim_wide_draws_kernel + W2 episodes + W3 combine" if sim.wide else
                            "msim_launch = K1 msim_draws_kernel + K2 episodes + K3 combine + finalize") +
                           " (HIP events on the launch stream; conservative: the whole launch, not the draw kernel alone)",
