@@ -6,10 +6,13 @@
 // call per GPU through the C ABI (include/msim.h); with MSIM_GPUS > 1 the run range is split across
 // devices (one host thread per device) and the integer sums are added exactly as an all-reduce would.
 //
-// Build: make -C host     Run: ./host/msim_main [n_gpus]
+// Build: make -C host     Run: ./host/msim_main [n_gpus] [seed_base] [default|c5]
+// "c5" runs BASELINE configs[4] (2 pools + 1 024 small miners, integer weights summing to
+// W = 102 400, msim_config_create_weighted), which the reference's integer percentages cannot express.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -47,6 +50,17 @@ std::vector<Miner> SetupMiners()
     return miners;
 }
 
+/** BASELINE configs[4] network: weights out of C5_TOTAL_WEIGHT, all honest, 1 s. */
+static constexpr uint64_t C5_TOTAL_WEIGHT{102'400};
+std::vector<Miner> SetupLargeNetwork()
+{
+    std::vector<Miner> miners;
+    miners.emplace_back(0, 30'720, 1s);
+    miners.emplace_back(1, 29'696, 1s);
+    for (unsigned i = 0; i < 1'024; ++i) miners.emplace_back(2 + i, 41, 1s);
+    return miners;
+}
+
 static int die(const char *what, int rc)
 {
     std::fprintf(stderr, "%s: %s (%d)\n", what, msim_strerror(rc), rc);
@@ -55,7 +69,9 @@ static int die(const char *what, int rc)
 
 int main(int argc, char **argv)
 {
-    const auto miners{SetupMiners()};
+    const bool large = argc > 3 && std::string(argv[3]) == "c5";
+    const auto miners{large ? SetupLargeNetwork() : SetupMiners()};
+    const uint64_t total_weight = large ? C5_TOTAL_WEIGHT : 100;
     const int n_gpus = argc > 1 ? std::atoi(argv[1]) : 1;
     const int64_t duration_ms = std::chrono::duration_cast<std::chrono::milliseconds>(SIM_DURATION).count();
     const uint32_t seed_base = argc > 2 ? (uint32_t)std::strtoul(argv[2], nullptr, 10) : 1000u;
@@ -64,7 +80,8 @@ int main(int argc, char **argv)
     for (const auto &m : miners)
         desc.push_back({m.id, m.perc, (int64_t)m.propagation.count(), (uint8_t)(m.is_selfish ? 1 : 0)});
     msim_config *cfg = nullptr;
-    if (int rc = msim_config_create(desc.data(), (uint32_t)desc.size(), duration_ms, &cfg)) return die("config", rc);
+    if (int rc = msim_config_create_weighted(desc.data(), (uint32_t)desc.size(), duration_ms, total_weight, &cfg))
+        return die("config", rc);
 
     std::printf("Running %d simulations in parallel using %d GPU(s).\n", SIM_RUNS, n_gpus);
     std::vector<std::vector<msim_sums>> part(n_gpus, std::vector<msim_sums>(miners.size()));
@@ -101,8 +118,12 @@ int main(int argc, char **argv)
     for (size_t i = 0; i < miners.size(); ++i) {
         const auto &miner{miners[i]};
         const auto &stats{stats_total[i]};
-        std::printf("  - Miner %u (%llu%% of network hashrate) found %lld blocks i.e. ", miner.id,
-                    (unsigned long long)miner.perc, (long long)(stats.blocks_found / SIM_RUNS));
+        if (total_weight == 100)
+            std::printf("  - Miner %u (%llu%% of network hashrate) found %lld blocks i.e. ", miner.id,
+                        (unsigned long long)miner.perc, (long long)(stats.blocks_found / SIM_RUNS));
+        else
+            std::printf("  - Miner %u (%g%% of network hashrate) found %lld blocks i.e. ", miner.id,
+                        (double)miner.perc * 100.0 / (double)total_weight, (long long)(stats.blocks_found / SIM_RUNS));
         std::printf("%g%% of blocks. Stale rate: %g%%.", stats.blocks_share * 100 / SIM_RUNS,
                     stats.stale_rate * 100 / SIM_RUNS);
         if (miner.is_selfish) std::printf(" ('selfish mining' strategy)");

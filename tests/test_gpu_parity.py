@@ -265,3 +265,16 @@ def test_host_dropin_driver(msim):
     rows = [[s.blocks_found, s.stale_blocks, s.share_hi, s.share_lo, s.rate_hi, s.rate_lo] for s in res.sums]
     want = msim.report(miners, msim.sums_to_stats(rows), 32768).splitlines()
     assert out[2:] == want
+
+
+def test_host_dropin_driver_large_network(msim):
+    """host/msim_main c5: BASELINE configs[4] through the C++ drop-in (msim_config_create_weighted)."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(GOLD), "..", "host", "msim_main")
+    raw = subprocess.run([exe, "1", "1000", "c5"], capture_output=True, check=True).stdout
+    out = raw.decode().rstrip("\n").split("\n")
+    assert out[2] == "After running 32768 simulations for 365d each, on average:"
+    assert len(out) == 3 + 1026
+    assert out[3].startswith("  - Miner 0 (30% of network hashrate) found ")
+    assert out[5].startswith("  - Miner 2 (0.0400391% of network hashrate) found ")
