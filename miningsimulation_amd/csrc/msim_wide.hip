@@ -232,6 +232,13 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
     wave_sync();
     uint32_t *hout = a.hist + (size_t)r * m;
     for (uint32_t k = lane; k < m; k += 64) hout[k] = s.hist[k];
+    {  // this run's candidate slots on the dense W2 work list (one atomic per run)
+        const uint32_t cc0 = *s.cc, ccn = cc0 < a.rcap ? cc0 : a.rcap;
+        uint32_t base = 0;
+        if (lane == 0 && ccn) base = atomicAdd(&a.counts[0], ccn);
+        base = __shfl(base, 0, 64);
+        for (uint32_t c = lane; c < ccn; c += 64) a.work[base + c] = r * a.rcap + c;
+    }
     if (lane == 0) {
         const uint32_t cc = *s.cc;
         uint32_t *inf = a.info + (size_t)r * 4;
@@ -244,18 +251,13 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
 }
 
 // ---------------------------------------------------------------- W2
-// RETRY = false: every candidate with small capacities (WE_FAST, WA_FAST); RETRY = true: only the
-// candidates the first pass flagged WREC_RETRY, with the record format's full capacities.
 template <bool RETRY>
-__global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a)
+__device__ __forceinline__ void wide_episode_slot(const WideArgs &a, uint32_t slot)
 {
-    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t r = (uint32_t)(idx / a.rcap), c = (uint32_t)(idx % a.rcap);
-    if (r >= a.n) return;
+    const size_t idx = slot;
+    const uint32_t r = (uint32_t)(idx / a.rcap);
     const uint32_t *inf = a.info + (size_t)r * 4;
-    if (c >= inf[2]) return;
     uint32_t *rec = a.recs + idx * WREC_WORDS;
-    if (RETRY && !(rec[1] & WREC_RETRY)) return;
     const WideCand e = a.cand[idx];
     if (inf[3] != 0 || e.block >= inf[0]) {  // failed run, or a block past the end of the run
         rec[0] = e.block + 1;
@@ -272,6 +274,7 @@ __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a
         if (o.flags & WREC_RETRY) o.flags = WREC_ERR;
     } else {
         wide_episode<WE_FAST, WA_FAST>(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
+        if (o.flags & WREC_RETRY) a.retry[atomicAdd(&a.counts[1], 1u)] = slot;
     }
     rec[0] = o.end;
     rec[1] = o.flags;
@@ -280,6 +283,19 @@ __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a
         rec[4 + 3 * i] = o.gid[i];
         rec[5 + 3 * i] = o.dF[i];
         rec[6 + 3 * i] = o.dS[i];
+    }
+}
+
+// RETRY = false: every candidate with small capacities (WE_FAST, WA_FAST); RETRY = true: only the
+// candidates the first pass flagged WREC_RETRY, with the record format's full capacities.
+// Grid-stride over the dense lists W1 / the first pass built (every thread of a wave has real work).
+template <bool RETRY>
+__global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a)
+{
+    const uint32_t total = RETRY ? a.counts[1] : a.counts[0];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+        const uint32_t slot = RETRY ? a.retry[i] : a.work[i];
+        wide_episode_slot<RETRY>(a, slot);
     }
 }
 
@@ -458,6 +474,9 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
     a.lanes = (WideLane *)(ws + L.lanes_off);
     a.cand = (WideCand *)(ws + L.cand_off);
     a.recs = (uint32_t *)(ws + L.recs_off);
+    a.work = (uint32_t *)(ws + L.work_off);
+    a.retry = (uint32_t *)(ws + L.retry_off);
+    a.counts = (uint32_t *)(ws + L.counts_off);
     const size_t l1 = wide_w1_lds(a.m), l3 = wide_w3_lds(a.m, a.rcap, a.nch);
     if (l3 > 160 * 1024) return hipErrorInvalidValue;
     for (uint64_t off = 0; off < out.n_total; off += L.nr) {
@@ -470,12 +489,14 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
             w1_events->push_back(ee);
             (void)hipEventRecord(eb, s);
         }
+        if (hipMemsetAsync(a.counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
         hipLaunchKernelGGL(msim_wide_draws_kernel, dim3((cn + 3) / 4), dim3(256), l1, s, a);
         if (ee) (void)hipEventRecord(ee, s);
-        const size_t nthreads = (size_t)cn * a.rcap;
-        const dim3 g2((unsigned)((nthreads + 255) / 256));
-        hipLaunchKernelGGL(msim_wide_episode_kernel<false>, g2, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(msim_wide_episode_kernel<true>, g2, dim3(256), 0, s, a);
+        // W2 grid: ~rho * blocks candidates per run, grid-stride beyond 16 384 workgroups
+        const double est = (double)cn * a.rcap * 0.6;
+        const unsigned g2 = (unsigned)(est / 256 < 16384 ? est / 256 + 1 : 16384);
+        hipLaunchKernelGGL(msim_wide_episode_kernel<false>, dim3(g2), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(msim_wide_episode_kernel<true>, dim3(64), dim3(256), 0, s, a);
         WideOut o = out;
         o.rel_begin = (uint32_t)off;
         uint32_t g3 = (cn + 3) / 4;

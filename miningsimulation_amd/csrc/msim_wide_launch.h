@@ -33,6 +33,9 @@ struct WideArgs {
     WideLane *lanes;  // [nr][1 + nch][64]
     WideCand *cand;   // [nr][rcap]
     uint32_t *recs;   // [nr][rcap][WREC_WORDS]
+    uint32_t *work;   // [nr * rcap] dense list of candidate slots (r * rcap + c) for W2
+    uint32_t *retry;  // [nr * rcap] slots the first W2 pass flagged WREC_RETRY
+    uint32_t *counts; // [2]: work entries, retry entries (zeroed per slice)
 };
 
 struct WideOut {
@@ -48,7 +51,7 @@ struct WideOut {
 struct WideLayout {
     uint32_t nr, rcap;
     WideGeom g;
-    size_t hist_off, info_off, tlast_off, lanes_off, cand_off, recs_off, total;
+    size_t hist_off, info_off, tlast_off, lanes_off, cand_off, recs_off, work_off, retry_off, counts_off, total;
 };
 
 // rho = P(a block is not fast) = sum_k w_k/W * P(I <= prop_k).
@@ -63,7 +66,7 @@ inline WideLayout wide_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     if (rc > 32000.0) rc = 32000.0;  // slot index fits 15 bits in the combine
     L.rcap = (uint32_t)rc;
     const double per_run = m * 4.0 + 16 + 8 + (1.0 + L.g.nch) * 64 * sizeof(WideLane) +
-                           L.rcap * (sizeof(WideCand) + 4.0 * WREC_WORDS) + 64;
+                           L.rcap * (sizeof(WideCand) + 4.0 * WREC_WORDS + 8.0) + 64;
     uint64_t cap = (uint64_t)(budget / per_run) / 256 * 256;
     if (cap < 256) cap = 256;
     const uint64_t want = (n_runs + 3) / 4 * 4;
@@ -81,6 +84,12 @@ inline WideLayout wide_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     o = al(o + (size_t)L.nr * L.rcap * sizeof(WideCand));
     L.recs_off = o;
     o = al(o + (size_t)L.nr * L.rcap * WREC_WORDS * 4);
+    L.work_off = o;
+    o = al(o + (size_t)L.nr * L.rcap * 4);
+    L.retry_off = o;
+    o = al(o + (size_t)L.nr * L.rcap * 4);
+    L.counts_off = o;
+    o = al(o + 8);
     L.total = o;
     return L;
 }
