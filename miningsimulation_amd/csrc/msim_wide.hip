@@ -347,39 +347,45 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             }
         }
         wave_sync();
-        // chain the episodes whose first block is reached quiet: a serial walk over the sorted list in
-        // LDS marks them (bit 15 of the slot field), then all lanes apply the marked episodes' deltas
+        // chain the episodes whose first block is reached quiet: 64 sorted entries at a time go into the
+        // lanes' registers, a wave-uniform walk reads them with v_readlane (no LDS round trip per step) and
+        // sets a 64-bit mask of the applied ones, then those lanes apply their sparse deltas (LDS atomics)
         uint32_t cursor = 0;
-        bool run_ended = false;
-        if (ok) {
-            for (uint32_t i = 0; i < cc; ++i) {
-                const uint32_t sblk = KB[i];
-                if (sblk >= n_end) break;
-                if (sblk < cursor) continue;
-                const uint32_t kf = KF[i], fl = kf >> 16;
-                if (fl & (WREC_ERR | WREC_SKIP | WREC_RETRY)) {
-                    ok = false;
+        bool run_ended = false, stop = !ok;
+        for (uint32_t base0 = 0; base0 < cc && !stop; base0 += 64) {
+            const uint32_t i = base0 + lane;
+            const bool valid = i < cc;
+            const uint32_t kb = valid ? KB[i] : 0xFFFFFFFFu, ke = valid ? KE[i] : 0u, kf = valid ? KF[i] : 0u;
+            const uint32_t lim = (cc - base0) < 64 ? (cc - base0) : 64;
+            uint64_t applied = 0;
+            for (uint32_t j = 0; j < lim; ++j) {
+                const uint32_t sblk = (uint32_t)__builtin_amdgcn_readlane((int)kb, (int)j);
+                if (sblk >= n_end) {
+                    stop = true;
                     break;
                 }
-                if (lane == 0) KF[i] = kf | 0x8000u;
-                cursor = KE[i];
+                if (sblk < cursor) continue;
+                const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)kf, (int)j) >> 16;
+                if (fl & (WREC_ERR | WREC_SKIP | WREC_RETRY)) {
+                    ok = false;
+                    stop = true;
+                    break;
+                }
+                applied |= 1ull << j;
+                cursor = (uint32_t)__builtin_amdgcn_readlane((int)ke, (int)j);
                 if (fl & WREC_ENDED) {
                     run_ended = true;
+                    stop = true;
                     break;
                 }
             }
-        }
-        wave_sync();
-        if (ok) {
-            for (uint32_t i = lane; i < cc; i += 64) {
-                const uint32_t kf = KF[i];
-                if (!(kf & 0x8000u)) continue;
-                const uint32_t *rec = a.recs + ((size_t)r * a.rcap + (kf & 0x7FFFu)) * WREC_WORDS;
+            if (ok && ((applied >> lane) & 1ull)) {
+                const uint32_t *rec = a.recs + ((size_t)r * a.rcap + (kf & 0xFFFFu)) * WREC_WORDS;
                 const uint32_t ne = rec[2];
-                for (uint32_t j = 0; j < ne; ++j) {
-                    const uint32_t g = rec[4 + 3 * j];
-                    atomicAdd(&F[g], rec[5 + 3 * j]);
-                    atomicAdd(&S[g], rec[6 + 3 * j]);
+                for (uint32_t q = 0; q < ne; ++q) {
+                    const uint32_t g = rec[4 + 3 * q];
+                    atomicAdd(&F[g], rec[5 + 3 * q]);
+                    atomicAdd(&S[g], rec[6 + 3 * q]);
                 }
             }
         }
