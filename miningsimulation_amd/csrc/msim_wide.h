@@ -26,8 +26,8 @@
 // PickFinder for integer weights w_k summing to W (W = 100 is exactly the reference's
 // percentages, simulation.h:18,213-221): q = floor(u / MULT), MULT = (2^64-1)/W, finder = first k with
 // cum_k > q. q is p1 = floor(u*W / 2^64) or p1 + 1 (one 64x64 high multiply and one compare, as in
-// msim_fastdraw.h); the first candidate k comes from a 1 024-entry bucket table indexed by u's top bits,
-// then a short scan of the cumulative table in LDS.
+// msim_fastdraw.h); the first candidate k comes from a 4 096-entry u16 bucket table indexed by u's top
+// bits, then a short scan of the packed cumulative-weight / fast-threshold table in LDS.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
