@@ -69,3 +69,50 @@ def test_gpu_c5_stale_rates_vs_model(msim):
     mod = np.array(msim.model.stale_rates([x / 102400 for x in w], 1.0))
     assert np.all(np.abs(rate[:2] / mod[:2] - 1) < 0.10), (rate[:2], mod[:2])
     assert abs(rate[2:].mean() / mod[2:].mean() - 1) < 0.25, (rate[2:].mean(), mod[2:].mean())
+
+
+def test_gpu_miner_picker_small_big_full_size(msim):
+    """test.cpp:68-119 MinerPickerSmallBig at its own size: 10^4 x 10^3 x 100 = 10^9 picks over miners
+    {12, 18, 20, 15, 35} %. The reference prints the sample mean of blocks per 100; its expectation is
+    100 * perc / 100 per miner (no skew with hashrate). Here: the total counts, within 5 sigma of a
+    multinomial(10^9, perc)."""
+    perc = [12, 18, 20, 15, 35]
+    n = 1_000_000_000
+    c = msim.sample_picks(_sim(msim, perc), 20240601, n)
+    assert c[-1] == 0 and int(c.sum()) == n
+    for k, pc in enumerate(perc):
+        p = pc / 100
+        mean_per_100 = float(c[k]) / n * 100  # the reference's "sample mean" (blocks per 100 picks)
+        sigma = (p * (1 - p) / n) ** 0.5 * 100
+        assert abs(mean_per_100 - pc) < 5 * sigma, (k, mean_per_100)
+
+
+def test_gpu_simple_sim_full_size(msim, oracle):
+    """test.cpp:122-187 SimpleSim at its own size: 100 samples x 100 runs of two weeks
+    (BLOCK_INTERVAL * 144 * 14), miners {12, 18, 20, 15, 35} %, propagation 0. The reference steps time
+    in 1 s increments and prints, per miner, the sample mean of BlocksFoundShare (expected: perc) and the
+    std dev of the sample mean. Here the same network runs through the event-driven device path
+    (msim_run; exact block times rather than 1 s steps, and without test.cpp's quirks of dropping the
+    genesis block on chain.clear() and never resetting stale_blocks), so the check is statistical:
+    sample means within 5 sigma of perc, the std dev of the sample means close to the binomial value,
+    and no stale blocks beyond same-millisecond ties. The first 64 runs are bit-exact vs the oracle."""
+    perc = [12, 18, 20, 15, 35]
+    dur = 600_000 * 144 * 14
+    sim = msim.Simulation([msim.Miner(k, w, 0) for k, w in enumerate(perc)], duration_ms=dur)
+    n_samples, n_size = 100, 100
+    res = sim.run(n_samples * n_size, 0, 1000, 0, per_run=True)
+    f, st, _, _ = oracle.run_batch(perc, [0] * 5, [False] * 5, dur, 64, 0, 1000, threads=16)
+    assert np.array_equal(res.found[:64].astype(np.int64), f)
+    assert np.array_equal(res.stale[:64].astype(np.int64), st)
+    share = res.found.astype(np.float64) / res.best_height.astype(np.float64)[:, None]
+    means = share.reshape(n_samples, n_size, 5).mean(axis=1)  # [sample, miner]
+    blocks = float(res.best_height.mean())
+    assert abs(blocks - 2016) < 5 * (2016 ** 0.5) / (n_samples * n_size) ** 0.5
+    for k, pc in enumerate(perc):
+        p = pc / 100
+        sm = means[:, k].mean()
+        sd = means[:, k].std()
+        sd_expect = (p * (1 - p) / (blocks * n_size)) ** 0.5
+        assert abs(sm - p) < 5 * sd_expect / n_samples ** 0.5, (k, sm)
+        assert 0.7 * sd_expect < sd < 1.3 * sd_expect, (k, sd, sd_expect)
+    assert int(res.stale.sum()) <= 1e-4 * int(res.found.sum())
