@@ -5,17 +5,27 @@
 
 namespace msim {
 
-__global__ void msim_finalize(const uint64_t *__restrict__ partials, uint32_t nparts, uint32_t nvals,
-                              uint64_t *__restrict__ out, const uint32_t *__restrict__ retry_count,
-                              const uint32_t *__restrict__ fail_count, const uint32_t retry_cap,
-                              uint32_t *__restrict__ status)
+// One workgroup per summed value: the lanes stride over the workgroup partials, then a wave
+// butterfly and the 4 waves through LDS (integer sums, so the result is order-independent). A single
+// workgroup walking the partials serially spent ~64 us per launch on dependent loads.
+__global__ __launch_bounds__(TPB) void msim_finalize(const uint64_t *__restrict__ partials, uint32_t nparts,
+                                                     uint32_t nvals, uint64_t *__restrict__ out,
+                                                     const uint32_t *__restrict__ retry_count,
+                                                     const uint32_t *__restrict__ fail_count, const uint32_t retry_cap,
+                                                     uint32_t *__restrict__ status)
 {
-    for (uint32_t i = threadIdx.x; i < nvals; i += blockDim.x) {
-        uint64_t s = 0;
-        for (uint32_t b = 0; b < nparts; ++b) s += partials[(size_t)b * nvals + i];
-        out[i] = s;
+    __shared__ uint64_t red[TPB / 64];
+    const uint32_t i = blockIdx.x;
+    if (i < nvals) {
+        unsigned long long s = 0;
+        for (uint32_t b = threadIdx.x; b < nparts; b += TPB) s += partials[(size_t)b * nvals + i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) out[i] = red[0] + red[1] + red[2] + red[3];
     }
-    if (threadIdx.x == 0 && status) {
+    if (i == 0 && threadIdx.x == 0 && status) {
         const uint32_t rc = *retry_count;
         status[0] = rc;
         status[1] = *fail_count + (rc > retry_cap ? rc - retry_cap : 0u);
@@ -39,7 +49,7 @@ hipError_t launch_finalize(const uint64_t *partials, uint32_t nparts, uint32_t n
                            const uint32_t *retry_count, const uint32_t *fail_count, uint32_t retry_cap,
                            uint32_t *status, hipStream_t stream)
 {
-    hipLaunchKernelGGL(msim_finalize, dim3(1), dim3(TPB), 0, stream, partials, nparts, nvals, out, retry_count,
+    hipLaunchKernelGGL(msim_finalize, dim3(nvals > 0 ? nvals : 1), dim3(TPB), 0, stream, partials, nparts, nvals, out, retry_count,
                        fail_count, retry_cap, status);
     return hipGetLastError();
 }
