@@ -30,13 +30,14 @@ extern "C" {
 #define MSIM_OK 0
 #define MSIM_E_INVALID (-1)  /* bad argument (null pointer, n == 0, negative duration/propagation) */
 #define MSIM_E_WEIGHTS (-2)  /* weights do not add up to 100 (or total_weight): the reference asserts */
-#define MSIM_E_SELFISH (-3)  /* more than one selfish miner (device path supports at most one) */
+#define MSIM_E_SELFISH (-3)  /* more than 4 selfish miners, or a selfish miner in a network of > 15 miners */
 #define MSIM_E_MINERS (-4)   /* too many miners (see MSIM_MAX_*_MINERS), or duplicate miner ids */
 #define MSIM_E_HIP (-5)      /* HIP runtime error (no device, launch failure, out of memory) */
 #define MSIM_E_CAPACITY (-6) /* a run exceeded the compact state's capacity even on the retry kernel */
 #define MSIM_E_PICK (-7)     /* PickFinder fell through (simulation.h:220 assert): percentages < 100 */
 
 #define MSIM_MAX_MINERS 15        /* networks with a selfish miner (compact per-lane state) */
+#define MSIM_MAX_SELFISH 4        /* selfish miners per network (entity engine, msim_sel.h) */
 #define MSIM_MAX_WIDE_MINERS 4096 /* honest networks (large-network pipeline, BASELINE configs[4]) */
 
 typedef struct msim_miner {
@@ -77,7 +78,8 @@ int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms
  * total_weight W < 2^31, and PickFinder uses UINT64_MAX / W in place of PERC_MULTIPLIER
  * (simulation.h:18, 217). W = 100 is exactly msim_config_create. Honest networks of more than
  * MSIM_MAX_MINERS miners (up to MSIM_MAX_WIDE_MINERS), or with W != 100, run on the large-network
- * pipeline; a selfish miner is supported only with W = 100 and n <= MSIM_MAX_MINERS. */
+ * pipeline; networks with selfish miners (up to MSIM_MAX_SELFISH of them, any W) need
+ * n <= MSIM_MAX_MINERS and run on the entity engine. */
 int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
                                 msim_config **out);
 /* 1 when the config runs on the large-network pipeline (set MSIM_FORCE_WIDE=1 in the environment before
@@ -97,8 +99,8 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
 
 /* Device-resident launch on the current HIP device and the given hipStream_t (NULL = default).
  * d_sums: M msim_sums in device memory (overwritten). d_per_run / d_best_height: device buffers or NULL.
- * d_status: 2 uint32_t in device memory: [0] = runs that needed the retry kernel, [1] = runs that
- * failed even there (each failed run contributes nothing to d_sums).
+ * d_status: 2 uint32_t in device memory (required): [0] = runs that needed the retry kernel, [1] = runs
+ * that failed even there (each failed run contributes nothing to d_sums: check it before using d_sums).
  * d_workspace / workspace_bytes: scratch from msim_workspace_bytes(); the call does no allocation
  * and no synchronisation, so it can be captured into a hipGraph. */
 size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs);
@@ -143,10 +145,14 @@ int msim_sweep_run(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_pe
  * elapsed milliseconds and the number of launches since the last enable/read, and clears them. */
 int msim_timing_enable(int on);
 int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches);
+/* Same, plus the entity engine's stage (networks with selfish miners: the E1 kernels of every slice;
+ * draws_ms is then the word-draw kernel D1). */
+int msim_timing_read_stages(double *draws_ms, double *engine_ms, double *launch_ms, uint32_t *launches);
 
 /* How msim_launch will execute n_runs of this config on the current device. */
 typedef struct msim_pipeline_layout {
-    uint32_t uses_pipeline;   /* 1: event-skipping pipeline (honest network); 0: per-lane kernel */
+    uint32_t uses_pipeline;   /* 1: event-skipping pipeline (honest network); 2: large-network pipeline;
+                                 3: entity engine (selfish miners); 0: per-lane kernel */
     uint32_t slice_runs;      /* runs per pipeline slice */
     uint32_t segment_blocks;  /* blocks per draw-kernel worker */
     uint32_t segments;        /* workers per run */

@@ -21,6 +21,7 @@ MSIM_E_HIP = -5
 MSIM_E_CAPACITY = -6
 MSIM_E_PICK = -7
 MSIM_MAX_MINERS = 15
+MSIM_MAX_SELFISH = 4
 
 # Every symbol include/msim.h declares (checked by tests/test_abi.py).
 EXPORTED = (
@@ -38,6 +39,7 @@ EXPORTED = (
     "msim_sums_to_stats",
     "msim_timing_enable",
     "msim_timing_read",
+    "msim_timing_read_stages",
     "msim_pipeline_info",
     "msim_sweep_create",
     "msim_sweep_destroy",
@@ -140,6 +142,9 @@ def _load() -> ctypes.CDLL:
     lib.msim_timing_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(u32)]
     lib.msim_timing_read.restype = ctypes.c_int
+    lib.msim_timing_read_stages.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32)]
+    lib.msim_timing_read_stages.restype = ctypes.c_int
     lib.msim_pipeline_info.argtypes = [vp, u64, ctypes.POINTER(MsimPipelineLayout)]
     lib.msim_pipeline_info.restype = ctypes.c_int
     lib.msim_sweep_create.argtypes = [ctypes.POINTER(vp), u32, ctypes.POINTER(vp)]

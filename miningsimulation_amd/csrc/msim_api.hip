@@ -16,6 +16,7 @@
 #include "../../include/msim.h"
 #include "msim_jump.h"
 #include "msim_kernels.h"
+#include "msim_sel_launch.h"
 #include "msim_wide_launch.h"
 
 namespace {
@@ -45,6 +46,11 @@ struct msim_config {
     std::vector<uint64_t> wperc;
     std::vector<int64_t> wprop;
     std::vector<std::pair<int, void *>> wtables;  // per device: pick, fast-threshold, prop, log, jump tables
+    // Networks with selfish miners (msim_sel.h entity engine): parameter block, capacity class.
+    bool sel = false;
+    msim::SelParams sp;
+    uint32_t sel_caps = msim::SEL_SMALL;
+    std::vector<std::pair<int, void *>> stables;  // per device: SelParams + point list {0}
 };
 
 // A parameter sweep (BASELINE configs[3]): the points' parameter blocks, uploaded per device on first use.
@@ -54,6 +60,18 @@ struct msim_sweep {
     bool self;
     std::mutex mu;
     std::vector<std::pair<int, void *>> dev;  // (device, SimParams[n_points])
+    // Entity-engine sweeps (some point has a selfish miner): every point's SelParams, the points grouped
+    // by (capacity class, selfish class), one draw pass per slice shared by all points.
+    bool sel = false;
+    int64_t max_duration = 0;
+    std::vector<msim::SelParams> sps;
+    struct Group {
+        uint32_t caps, nscls;
+        std::vector<uint32_t> points;
+    };
+    std::vector<Group> groups;
+    std::vector<std::pair<int, void *>> sdev;  // (device, SelParams[n_points] + point lists)
+    const msim_config *tab_cfg = nullptr;      // config whose log / jump tables the draws use
 };
 
 namespace {
@@ -158,6 +176,7 @@ struct Timing {
     bool on = false;
     std::vector<hipEvent_t> k1;      // (begin, end) pairs around K1
     std::vector<hipEvent_t> launch;  // (begin, end) pairs around msim_launch
+    std::vector<hipEvent_t> engine;  // (begin, end) pairs around the entity engine (E1) of each slice
     uint32_t launches = 0;
 };
 Timing &timing()
@@ -276,6 +295,193 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
     return MSIM_OK;
 }
 
+// ---------------------------------------------------------------- entity-engine path (msim_sel_launch.h)
+constexpr double SEL_SLICE_BUDGET = 32.0 * (1ull << 30);  // word stream per slice (bytes)
+
+uint32_t word_draw_slots()
+{
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        msim::word_draws_blocks_per_cu(&blocks) != hipSuccess || cus <= 0 || blocks <= 0)
+        return 8192;
+    return (uint32_t)(cus * blocks * 4);
+}
+
+struct SelWs {
+    msim::SelLayout L;
+    uint32_t wpp, err_cap;
+    size_t counts_off, partials_off, retry_off, list_off, words_off, total;
+};
+
+SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
+{
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    SelWs w;
+    w.L = msim::sel_layout_for(duration_ms, rpp, SEL_SLICE_BUDGET, word_draw_slots());
+    w.wpp = (uint32_t)((rpp + msim::TPB - 1) / msim::TPB);
+    w.err_cap = (uint32_t)(rpp * np);  // every lane can be retried: the list never overflows
+    const size_t nv = 6 * (size_t)m;
+    w.counts_off = 0;
+    w.partials_off = 256;
+    w.retry_off = al(w.partials_off + (size_t)np * w.wpp * nv * 8);
+    w.list_off = al(w.retry_off + (size_t)np * nv * 8);
+    w.words_off = al(w.list_off + (size_t)w.err_cap * 4);
+    w.total = al(w.words_off + w.L.words_bytes);
+    return w;
+}
+
+// One SelParams for a validated network (weights summing to W, <= MSIM_MAX_MINERS miners).
+void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t W, msim::SelParams *sp)
+{
+    using namespace msim;
+    memset(sp, 0, sizeof(*sp));
+    sp->duration_ms = duration_ms;
+    sp->W = (uint32_t)W;
+    sp->mult = 0xFFFFFFFFFFFFFFFFull / W;
+    sp->m = n;
+    for (int i = 0; i < SEL_MAXS; ++i) sp->sids[i] = SEL_NONE;
+    uint64_t c = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        c += miners[k].perc;
+        sp->cum[k] = c;
+        sp->prop[k] = miners[k].propagation_ms;
+        if (miners[k].is_selfish) sp->sids[sp->ns++] = k;
+    }
+    // word code -> finder: W = 100 words carry q = floor(u / PERC_MULTIPLIER) (first k with cum_k > q,
+    // simulation.h:217-218); weighted words carry the finder itself.
+    for (uint32_t q = 0; q < SEL_LUT; ++q) {
+        uint32_t f = 15;
+        if (W == 100) {
+            for (uint32_t k = 0; k < n && q <= 100; ++k)
+                if (sp->cum[k] > q) {
+                    f = k;
+                    break;
+                }
+        } else if (q < n) {
+            f = q;
+        }
+        sp->lut[q] = (uint8_t)f;
+    }
+}
+
+struct SelGroupDev {
+    uint32_t caps, nscls, nlist;
+    const uint32_t *plist;
+};
+
+// The slice loop of one launch: D1 (words) -> E1 per group -> E2 (retries) -> F.
+int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const std::vector<SelGroupDev> &groups,
+                    const msim::WordArgs &wt, const SelWs &w, char *ws, uint64_t run_begin, uint64_t rpp,
+                    uint32_t seed_base, void *d_sums, void *d_per_run, void *d_best_height, void *d_status, hipStream_t s,
+                    std::vector<hipEvent_t> *draw_events, std::vector<hipEvent_t> *engine_events)
+{
+    using namespace msim;
+    uint32_t *counts = (uint32_t *)(ws + w.counts_off);
+    uint64_t *retry = (uint64_t *)(ws + w.retry_off);
+    if (hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(retry, 0, (size_t)np * 6 * m * 8, s) != hipSuccess)
+        return MSIM_E_HIP;
+    SelArgs a;
+    a.pts = d_pts;
+    a.rpp = (uint32_t)rpp;
+    a.wpp = w.wpp;
+    a.run_begin = run_begin;
+    a.seed_base = seed_base;
+    a.nr = w.L.nr;
+    a.nb = w.L.nb;
+    a.words = (const uint32_t *)(ws + w.words_off);
+    a.partials = (uint64_t *)(ws + w.partials_off);
+    a.retry_sums = retry;
+    a.records = (uint32_t *)d_per_run;
+    a.best_h = (uint32_t *)d_best_height;
+    a.counts = counts;
+    a.err_list = (uint32_t *)(ws + w.list_off);
+    a.err_cap = w.err_cap;
+    a.force_retry = getenv("MSIM_SEL_FORCE_RETRY") != nullptr ? 1u : 0u;
+    WordArgs da = wt;
+    da.seed_base = seed_base;
+    da.nr = w.L.nr;
+    da.seg = w.L.seg;
+    da.nseg = w.L.nseg;
+    da.words = (uint32_t *)(ws + w.words_off);
+    auto event = [&](std::vector<hipEvent_t> *v) -> hipEvent_t {
+        hipEvent_t e = nullptr;
+        if (v && hipEventCreate(&e) == hipSuccess) {
+            v->push_back(e);
+            (void)hipEventRecord(e, s);
+        }
+        return e;
+    };
+    uint32_t max_ns = 1;
+    for (const auto &g : groups) max_ns = g.nscls > max_ns ? g.nscls : max_ns;
+    for (uint64_t s0 = 0; s0 < rpp; s0 += w.L.nr) {
+        const uint32_t sn = (uint32_t)((rpp - s0) < w.L.nr ? (rpp - s0) : w.L.nr);
+        da.run_begin = run_begin + s0;
+        event(draw_events);
+        if (launch_word_draws(da, s) != hipSuccess) return MSIM_E_HIP;
+        event(draw_events);
+        a.s0 = (uint32_t)s0;
+        a.sn = sn;
+        event(engine_events);
+        for (const auto &g : groups) {
+            if (!g.nlist) continue;
+            a.plist = g.plist;
+            a.nlist = g.nlist;
+            if (launch_sel(a, m, g.nscls, g.caps, s) != hipSuccess) return MSIM_E_HIP;
+        }
+        event(engine_events);
+    }
+    a.s0 = 0;
+    a.sn = 0;
+    if (launch_sel_retry(a, m, max_ns, s) != hipSuccess) return MSIM_E_HIP;
+    if (launch_sel_finalize(a.partials, np, w.wpp, 6 * m, retry, (uint64_t *)d_sums, counts, (uint32_t *)d_status, s) !=
+        hipSuccess)
+        return MSIM_E_HIP;
+    return MSIM_OK;
+}
+
+// Device copy of a config's SelParams and the point list {0}.
+int sel_config_tables(msim_config *c, const msim::SelParams **pts, const uint32_t **plist)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
+    std::lock_guard<std::mutex> g(c->mu);
+    void *d = nullptr;
+    for (const auto &t : c->stables)
+        if (t.first == dev) d = t.second;
+    const size_t pb = (sizeof(msim::SelParams) + 255) / 256 * 256;
+    if (!d) {
+        std::vector<char> h(pb + 256, 0);
+        memcpy(h.data(), &c->sp, sizeof(msim::SelParams));
+        if (hipMalloc(&d, h.size()) != hipSuccess) return MSIM_E_HIP;
+        if (hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(d);
+            return MSIM_E_HIP;
+        }
+        c->stables.push_back({dev, d});
+    }
+    *pts = (const msim::SelParams *)d;
+    *plist = (const uint32_t *)((const char *)d + pb);
+    return MSIM_OK;
+}
+
+// Word-draw arguments (tables for the slice geometry) of a network with SelParams sp.
+int sel_word_args(msim_config *tabc, const msim::SelParams &sp, const SelWs &w, msim::WordArgs *da)
+{
+    msim::PipeTables t;
+    const int rc = device_tables(tabc, w.L.seg, w.L.nseg, &t);
+    if (rc) return rc;
+    memset(da, 0, sizeof(*da));
+    da->logt = t.logt;
+    da->jump = t.jump;
+    da->mode = sp.W == 100 ? 0u : 1u;
+    da->W = sp.W;
+    da->m = sp.m;
+    da->mult = sp.mult;
+    for (int k = 0; k < msim::MAXM; ++k) da->cum[k] = sp.cum[k];
+    return MSIM_OK;
+}
+
 // Validate a miner list with integer weights summing to total_weight and build the config.
 int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
                        msim_config **out)
@@ -300,10 +506,13 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     }
     // "Must add up to 1" (main.cpp:43); anything else makes PickFinder assert (simulation.h:220).
     if (total != total_weight) return MSIM_E_WEIGHTS;
-    if (nself > 1) return MSIM_E_SELFISH;
-    const bool narrow = n <= MSIM_MAX_MINERS && total_weight == 100;
+    // Selfish miners run on the entity engine (msim_sel.h): up to SEL_MAXS of them, in networks of up to
+    // MSIM_MAX_MINERS miners with any integer weights. The large-network path is honest-only.
+    if (nself > (uint32_t)msim::SEL_MAXS) return MSIM_E_SELFISH;
+    if (nself && n > MSIM_MAX_MINERS) return MSIM_E_SELFISH;
+    const bool sel = nself > 0;
+    const bool narrow = n <= MSIM_MAX_MINERS && (total_weight == 100 || sel);
     const bool force_wide = getenv("MSIM_FORCE_WIDE") != nullptr && nself == 0;
-    if (!narrow && nself) return MSIM_E_SELFISH;  // the large-network path is honest-only
     msim_config *c = new (std::nothrow) msim_config();
     if (!c) return MSIM_E_INVALID;
     c->n = n;
@@ -323,12 +532,28 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
             c->prop[k] = miners[k].propagation_ms;
             c->self[k] = miners[k].is_selfish ? 1 : 0;
         }
-        const int rc = msim::make_params(c->perc, c->prop, c->self, (int)n, duration_ms, &c->p);
-        if (rc) {
-            delete c;
-            return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
+        if (sel) {
+            c->sel = true;
+            build_sel_params(miners, n, duration_ms, total_weight, &c->sp);
+            int64_t maxp = 0;
+            for (uint32_t k = 0; k < n; ++k) maxp = miners[k].propagation_ms > maxp ? miners[k].propagation_ms : maxp;
+            c->sel_caps = maxp <= msim::SEL_SMALL_MAX_PROP ? msim::SEL_SMALL : msim::SEL_LARGE;
+            if (getenv("MSIM_SEL_LARGE")) c->sel_caps = msim::SEL_LARGE;
+            c->p.duration_ms = duration_ms;
+            c->p.m = (int32_t)n;
+            c->p.selfish = (int32_t)c->sp.sids[0];
+            for (int k = 0; k < msim::MAXM; ++k) {
+                c->p.prop[k] = k < (int)n ? miners[k].propagation_ms : 0;
+                c->p.thresh[k] = ~0ull;
+            }
+        } else {
+            const int rc = msim::make_params(c->perc, c->prop, c->self, (int)n, duration_ms, &c->p);
+            if (rc) {
+                delete c;
+                return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
+            }
         }
-        c->pipe_ok = c->p.selfish < 0 && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
+        c->pipe_ok = !sel && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
     } else {
         c->wide = true;
         c->pipe_ok = false;
@@ -404,6 +629,7 @@ void msim_config_destroy(msim_config *cfg)
     if (!cfg) return;
     for (const auto &t : cfg->tables) (void)hipFree(t.ptr);
     for (const auto &t : cfg->wtables) (void)hipFree(t.second);
+    for (const auto &t : cfg->stables) (void)hipFree(t.second);
     delete cfg;
 }
 
@@ -413,6 +639,7 @@ size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
 {
     if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
     if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
+    if (cfg->sel) return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total;
     size_t t = ws_layout(cfg->n, n_runs).total;
     if (cfg->pipe_ok) t += pipe_layout(cfg, n_runs).total;
     return t;
@@ -422,7 +649,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
                 void *d_per_run, void *d_best_height, void *d_status, void *d_workspace, size_t workspace_bytes,
                 void *stream)
 {
-    if (!cfg || !d_sums || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    if (!cfg || !d_sums || !d_status || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
     if (cfg->wide) {
         Timing &tm = timing();
         std::unique_lock<std::mutex> lk(tm.mu);
@@ -442,6 +669,38 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         const int rc = launch_wide_cfg(cfg, run_begin, n_runs, seed_base, d_sums, d_per_run, d_best_height, d_status,
                                        d_workspace, workspace_bytes, stream, w1);
         if (le) (void)hipEventRecord(le, (hipStream_t)stream);
+        return rc;
+    }
+    if (cfg->sel) {
+        const SelWs w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
+        if (workspace_bytes < w.total) return MSIM_E_INVALID;
+        msim_config *c = const_cast<msim_config *>(cfg);
+        const msim::SelParams *pts = nullptr;
+        const uint32_t *plist = nullptr;
+        int rc = sel_config_tables(c, &pts, &plist);
+        if (rc) return rc;
+        msim::WordArgs da;
+        rc = sel_word_args(c, cfg->sp, w, &da);
+        if (rc) return rc;
+        std::vector<SelGroupDev> groups{{cfg->sel_caps, msim::sel_ns_class(cfg->sp.ns), 1u, plist}};
+        Timing &tm = timing();
+        std::unique_lock<std::mutex> lk(tm.mu);
+        hipEvent_t lb = nullptr, le = nullptr;
+        hipStream_t s = (hipStream_t)stream;
+        const bool on = tm.on;
+        if (on) {
+            if (hipEventCreate(&lb) == hipSuccess && hipEventCreate(&le) == hipSuccess) {
+                tm.launch.push_back(lb);
+                tm.launch.push_back(le);
+                (void)hipEventRecord(lb, s);
+            }
+            tm.launches++;
+        } else {
+            lk.unlock();
+        }
+        rc = sel_launch_impl(cfg->n, 1, pts, groups, da, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
+                             d_per_run, d_best_height, d_status, s, on ? &tm.k1 : nullptr, on ? &tm.engine : nullptr);
+        if (le) (void)hipEventRecord(le, s);
         return rc;
     }
     const WsLayout l = ws_layout(cfg->n, n_runs);
@@ -619,12 +878,45 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
     w->m = cfgs[0] ? cfgs[0]->n : 0;
     w->self = false;
     for (uint32_t i = 0; i < n_points; ++i) {
-        if (!cfgs[i] || cfgs[i]->n != w->m || cfgs[i]->wide) {  // one miner count per sweep; narrow networks
+        // one miner count per sweep; narrow networks with percentages (the words are shared by all points)
+        if (!cfgs[i] || cfgs[i]->n != w->m || cfgs[i]->wide || cfgs[i]->total_weight != 100) {
             delete w;
             return MSIM_E_INVALID;
         }
         w->pts.push_back(cfgs[i]->p);
         w->self = w->self || cfgs[i]->p.selfish >= 0;
+        w->sel = w->sel || cfgs[i]->sel;
+    }
+    if (w->sel) {
+        // every point on the entity engine; points grouped by (capacity class, selfish class)
+        for (uint32_t i = 0; i < n_points; ++i) {
+            const msim_config *c = cfgs[i];
+            msim::SelParams sp;
+            uint32_t caps = c->sel_caps;
+            if (c->sel) {
+                sp = c->sp;
+            } else {
+                std::vector<msim_miner> ms(c->n);
+                int64_t maxp = 0;
+                for (uint32_t k = 0; k < c->n; ++k) {
+                    ms[k] = msim_miner{c->ids[k], c->perc[k], c->prop[k], 0};
+                    maxp = c->prop[k] > maxp ? c->prop[k] : maxp;
+                }
+                build_sel_params(ms.data(), c->n, c->p.duration_ms, 100, &sp);
+                caps = maxp <= msim::SEL_SMALL_MAX_PROP ? msim::SEL_SMALL : msim::SEL_LARGE;
+            }
+            w->sps.push_back(sp);
+            w->max_duration = sp.duration_ms > w->max_duration ? sp.duration_ms : w->max_duration;
+            const uint32_t nc = msim::sel_ns_class(sp.ns);
+            bool placed = false;
+            for (auto &g : w->groups)
+                if (g.caps == caps && g.nscls == nc) {
+                    g.points.push_back(i);
+                    placed = true;
+                }
+            if (!placed) w->groups.push_back({caps, nc, {i}});
+        }
+        w->tab_cfg = cfgs[0];
     }
     *out = w;
     return MSIM_OK;
@@ -634,12 +926,14 @@ void msim_sweep_destroy(msim_sweep *sw)
 {
     if (!sw) return;
     for (const auto &d : sw->dev) (void)hipFree(d.second);
+    for (const auto &d : sw->sdev) (void)hipFree(d.second);
     delete sw;
 }
 
 size_t msim_sweep_workspace_bytes(const msim_sweep *sw, uint64_t runs_per_point)
 {
     if (!sw || runs_per_point == 0 || runs_per_point * sw->pts.size() > MAX_LAUNCH_RUNS) return 0;
+    if (sw->sel) return sel_ws_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration).total;
     return sweep_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point).total;
 }
 
@@ -647,9 +941,48 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
                       void *d_sums, void *d_per_run, void *d_best_height, void *d_status, void *d_workspace,
                       size_t workspace_bytes, void *stream)
 {
-    if (!sw || !d_sums || !d_workspace || runs_per_point == 0) return MSIM_E_INVALID;
+    if (!sw || !d_sums || !d_status || !d_workspace || runs_per_point == 0) return MSIM_E_INVALID;
     const uint32_t np = (uint32_t)sw->pts.size();
     if (runs_per_point * np > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    if (sw->sel) {
+        const SelWs w = sel_ws_layout(sw->m, np, runs_per_point, sw->max_duration);
+        if (workspace_bytes < w.total) return MSIM_E_INVALID;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
+        msim_sweep *sm = const_cast<msim_sweep *>(sw);
+        void *d = nullptr;
+        const size_t pb = (np * sizeof(msim::SelParams) + 255) / 256 * 256;
+        {
+            std::lock_guard<std::mutex> g(sm->mu);
+            for (const auto &x : sm->sdev)
+                if (x.first == dev) d = x.second;
+            if (!d) {
+                std::vector<char> h(pb + (size_t)np * 4, 0);
+                memcpy(h.data(), sm->sps.data(), np * sizeof(msim::SelParams));
+                uint32_t *pl = (uint32_t *)(h.data() + pb);
+                for (const auto &gr : sm->groups)
+                    for (uint32_t p : gr.points) *pl++ = p;
+                if (hipMalloc(&d, h.size()) != hipSuccess) return MSIM_E_HIP;
+                if (hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                    (void)hipFree(d);
+                    return MSIM_E_HIP;
+                }
+                sm->sdev.push_back({dev, d});
+            }
+        }
+        std::vector<SelGroupDev> groups;
+        const uint32_t *pl = (const uint32_t *)((const char *)d + pb);
+        for (const auto &gr : sm->groups) {
+            groups.push_back({gr.caps, gr.nscls, (uint32_t)gr.points.size(), pl});
+            pl += gr.points.size();
+        }
+        msim::WordArgs da;
+        int rc = sel_word_args(const_cast<msim_config *>(sw->tab_cfg), sm->sps[0], w, &da);
+        if (rc) return rc;
+        return sel_launch_impl(sw->m, np, (const msim::SelParams *)d, groups, da, w, (char *)d_workspace, run_begin,
+                               runs_per_point, seed_base, d_sums, d_per_run, d_best_height, d_status,
+                               (hipStream_t)stream, nullptr, nullptr);
+    }
     const SweepLayout l = sweep_layout(sw->m, np, runs_per_point);
     if (workspace_bytes < l.total) return MSIM_E_INVALID;
     int dev = 0;
@@ -743,34 +1076,44 @@ int msim_timing_enable(int on)
     std::lock_guard<std::mutex> g(tm.mu);
     destroy_events(tm.k1);
     destroy_events(tm.launch);
+    destroy_events(tm.engine);
     tm.launches = 0;
     tm.on = on != 0;
     return MSIM_OK;
 }
 
-int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches)
+int msim_timing_read_stages(double *draws_ms, double *engine_ms, double *launch_ms, uint32_t *launches)
 {
-    if (!draws_ms || !launch_ms || !launches) return MSIM_E_INVALID;
+    if (!draws_ms || !engine_ms || !launch_ms || !launches) return MSIM_E_INVALID;
     Timing &tm = timing();
     std::lock_guard<std::mutex> g(tm.mu);
-    double d = 0, l = 0;
+    double acc[3] = {0, 0, 0};
     int rc = MSIM_OK;
-    for (int pass = 0; pass < 2; ++pass) {
-        std::vector<hipEvent_t> &v = pass ? tm.launch : tm.k1;
+    std::vector<hipEvent_t> *vs[3] = {&tm.k1, &tm.engine, &tm.launch};
+    for (int pass = 0; pass < 3; ++pass) {
+        std::vector<hipEvent_t> &v = *vs[pass];
         for (size_t i = 0; i + 1 < v.size(); i += 2) {
             float ms = 0;
             if (hipEventSynchronize(v[i + 1]) != hipSuccess || hipEventElapsedTime(&ms, v[i], v[i + 1]) != hipSuccess)
                 rc = MSIM_E_HIP;
-            (pass ? l : d) += ms;
+            acc[pass] += ms;
         }
     }
-    *draws_ms = d;
-    *launch_ms = l;
+    *draws_ms = acc[0];
+    *engine_ms = acc[1];
+    *launch_ms = acc[2];
     *launches = tm.launches;
     destroy_events(tm.k1);
     destroy_events(tm.launch);
+    destroy_events(tm.engine);
     tm.launches = 0;
     return rc;
+}
+
+int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches)
+{
+    double e = 0;
+    return msim_timing_read_stages(draws_ms, &e, launch_ms, launches);
 }
 
 int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_layout *out)
@@ -786,6 +1129,16 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
         out->segments = 64;
         out->blocks_per_run = L.g.B0 + 64ull * L.g.ST * L.g.nch;
         out->workspace_bytes = L.total;
+        return MSIM_OK;
+    }
+    if (cfg->sel) {
+        const SelWs w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
+        out->uses_pipeline = 3;
+        out->slice_runs = w.L.nr;
+        out->segment_blocks = w.L.seg;
+        out->segments = w.L.nseg;
+        out->blocks_per_run = w.L.nb;
+        out->workspace_bytes = w.total;
         return MSIM_OK;
     }
     if (!cfg->pipe_ok) return MSIM_OK;
@@ -891,7 +1244,7 @@ const char *msim_strerror(int code)
     case MSIM_OK: return "ok";
     case MSIM_E_INVALID: return "invalid argument";
     case MSIM_E_WEIGHTS: return "miner weights must be integers adding up to the total weight (100 for percentages)";
-    case MSIM_E_SELFISH: return "at most one selfish miner is supported on the device path";
+    case MSIM_E_SELFISH: return "at most 4 selfish miners, in networks of at most 15 miners, are supported on the device path";
     case MSIM_E_MINERS: return "too many miners (max 4096; networks with a selfish miner: 15) or duplicate miner ids";
     case MSIM_E_HIP: return "HIP runtime error";
     case MSIM_E_CAPACITY: return "a run exceeded the compact state capacity";

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include "msim_kernels.h"
+#include "msim_sel_launch.h"
 
 namespace msim {
 
@@ -103,6 +104,62 @@ hipError_t launch_sweep(const SweepArgs &a)
     default:
         return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, uint32_t caps, hipStream_t s)
+{
+    switch (m) {
+#define CASE(MM) \
+    case MM:     \
+        return launch_sel_m##MM(a, ns_class, caps, s);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s)
+{
+    switch (m) {
+#define CASE(MM) \
+    case MM:     \
+        return launch_sel_retry_m##MM(a, ns_class, s);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+// F: one workgroup per (point, value); lanes stride over the point's workgroup partials.
+__global__ __launch_bounds__(TPB) void msim_sel_finalize(const uint64_t *__restrict__ partials, uint32_t wpp,
+                                                         uint32_t nvals, const uint64_t *__restrict__ retry_sums,
+                                                         uint64_t *__restrict__ out, const uint32_t *__restrict__ counts,
+                                                         uint32_t *__restrict__ status)
+{
+    __shared__ uint64_t red[TPB / 64];
+    const uint32_t p = blockIdx.x / nvals, i = blockIdx.x % nvals;
+    unsigned long long s = 0;
+    for (uint32_t b = threadIdx.x; b < wpp; b += TPB) s += partials[((size_t)p * wpp + b) * nvals + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[(size_t)p * nvals + i] = red[0] + red[1] + red[2] + red[3] + retry_sums[(size_t)p * nvals + i];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && status) {
+        status[0] = counts[0];
+        status[1] = counts[1];
+    }
+}
+
+hipError_t launch_sel_finalize(const uint64_t *partials, uint32_t n_points, uint32_t wpp, uint32_t nvals,
+                               const uint64_t *retry_sums, uint64_t *out, const uint32_t *counts, uint32_t *status,
+                               hipStream_t s)
+{
+    hipLaunchKernelGGL(msim_sel_finalize, dim3(n_points * nvals), dim3(TPB), 0, s, partials, wpp, nvals, retry_sums, out,
+                       counts, status);
+    return hipGetLastError();
 }
 
 size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap)

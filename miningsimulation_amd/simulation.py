@@ -278,10 +278,12 @@ def timing_enable(on: bool = True) -> None:
 
 
 def timing_read() -> dict:
-    """Summed K1 / whole-launch milliseconds and launch count since the last enable/read (synchronises)."""
-    d, l, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
-    check(lib.msim_timing_read(ctypes.byref(d), ctypes.byref(l), ctypes.byref(n)), "msim_timing_read")
-    return {"draws_ms": d.value, "launch_ms": l.value, "launches": n.value}
+    """Summed draw-kernel / entity-engine / whole-launch milliseconds and the launch count since the last
+    enable/read (synchronises). draws_ms: K1 (honest pipeline) or D1 (entity engine); engine_ms: E1."""
+    d, e, l, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
+    check(lib.msim_timing_read_stages(ctypes.byref(d), ctypes.byref(e), ctypes.byref(l), ctypes.byref(n)),
+          "msim_timing_read_stages")
+    return {"draws_ms": d.value, "engine_ms": e.value, "launch_ms": l.value, "launches": n.value}
 
 
 def sums_to_stats(sums_rows: Iterable[Sequence[int]]) -> List[MinerStats]:

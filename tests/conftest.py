@@ -35,9 +35,10 @@ def native_tests():
     pipe = os.path.join(ROOT, "build", "libpipeline_host.so")
     chk = os.path.join(ROOT, "build", "draws_check")
     wide = os.path.join(ROOT, "build", "libwide_host.so")
-    if not all(os.path.exists(p) for p in (lib, chk, pipe, wide)):
+    sel = os.path.join(ROOT, "build", "libsel_host.so")
+    if not all(os.path.exists(p) for p in (lib, chk, pipe, wide, sel)):
         ge.build_native_tests()
-    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide}
+    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel}
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,118 @@
+// sel_host.cpp — TEST INFRASTRUCTURE: a host (CPU) build of the product's entity engine
+// (miningsimulation_amd/csrc/msim_sel.h) so its algorithm can be checked against the oracle on machines
+// without a GPU. Never part of the product path (libmsim.so is GPU-only).
+#include <stdint.h>
+#include <string.h>
+
+#include "../../miningsimulation_amd/csrc/msim_dispatch.h"
+#include "../../miningsimulation_amd/csrc/msim_sel.h"
+
+using namespace msim;
+
+namespace {
+
+struct HostEnv {
+    const int64_t *props;
+    uint32_t c[4][MAXM];
+    int64_t prop(uint32_t k) const { return props[k]; }
+    uint32_t get(int a, uint32_t k) const { return c[a][k]; }
+    void add(int a, uint32_t k, uint32_t v) { c[a][k] += v; }
+    void set(int a, uint32_t k, uint32_t v) { c[a][k] = v; }
+};
+
+// Draws exactly as the reference's loop makes them (simulation.h:205-221), through the same packed
+// word the device draw kernel writes: interval << 7 | q, q = floor(u / MULT), finder = first k with
+// cum_k > q (weights summing to W; W = 100 is PickFinder with PERC_MULTIPLIER).
+struct HostSrc {
+    Rng ri, rp;
+    const uint64_t *cum;  // cumulative weights
+    int m;
+    uint64_t W, mult;
+    bool next(uint32_t &I, uint32_t &k)
+    {
+        I = (uint32_t)next_interval(ri);
+        const uint64_t u = rng_next(rp);
+        const uint64_t q = u / mult;
+        uint32_t f = 0;
+        while ((int)f < m && cum[f] <= q) ++f;
+        k = f;  // == m: fell through (simulation.h:220)
+        return true;
+    }
+};
+
+template <int M, int NS, int NA, int NG, int NQ>
+void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
+{
+    HostEnv env;
+    env.props = prop;
+    memset(env.c, 0, sizeof(env.c));
+    Sel<M, NS, NA, NG, NQ> s;
+    s.init((uint32_t)M, sids);
+    s.run(env, src, D, o);
+}
+
+template <int M, int NS>
+void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
+{
+    if (caps == 0) run_one<M, NS, 2, 4, 2>(prop, sids, src, D, o);
+    else if (caps == 1) run_one<M, NS, 8, 16, 8>(prop, sids, src, D, o);
+    else if (caps == 2) run_one<M, NS, 1, 1, 1>(prop, sids, src, D, o);  // tiny: exercises the error paths
+#ifdef SEL_CAP_PROBE
+    else if (caps == 3) run_one<M, NS, 4, 4, 2>(prop, sids, src, D, o);
+    else if (caps == 4) run_one<M, NS, 2, 8, 2>(prop, sids, src, D, o);
+    else if (caps == 5) run_one<M, NS, 2, 4, 4>(prop, sids, src, D, o);
+    else if (caps == 6) run_one<M, NS, 3, 6, 3>(prop, sids, src, D, o);
+    else if (caps == 7) run_one<M, NS, 4, 8, 3>(prop, sids, src, D, o);
+    else if (caps == 8) run_one<M, NS, 3, 4, 2>(prop, sids, src, D, o);
+    else if (caps == 9) run_one<M, NS, 3, 6, 2>(prop, sids, src, D, o);
+#endif
+}
+
+}  // namespace
+
+// weights[m] summing to W, prop[m], selfish[m]; caps 0 = fast kernel capacities, 1 = retry, 2 = tiny.
+extern "C" int sel_run(const uint64_t *weights, const int64_t *prop, const uint8_t *selfish, int m, uint64_t W,
+                       int64_t duration_ms, uint32_t seed_i, uint32_t seed_p, int caps, uint32_t *found,
+                       uint32_t *stale, uint32_t *best_height, uint32_t *err)
+{
+    if (m < 1 || m > MAXM || W == 0) return -1;
+    uint64_t cum[MAXM];
+    uint64_t c = 0;
+    uint32_t sids[SEL_MAXS];
+    int ns = 0;
+    for (int k = 0; k < SEL_MAXS; ++k) sids[k] = SEL_NONE;
+    for (int k = 0; k < m; ++k) {
+        c += weights[k];
+        cum[k] = c;
+        if (selfish[k]) {
+            if (ns == SEL_MAXS) return -3;
+            sids[ns++] = (uint32_t)k;
+        }
+    }
+    if (c != W) return -2;
+    HostSrc src;
+    src.ri = rng_seed(seed_i);
+    src.rp = rng_seed(seed_p);
+    src.cum = cum;
+    src.m = m;
+    src.W = W;
+    src.mult = 0xFFFFFFFFFFFFFFFFull / W;
+    SelOut o;
+    memset(&o, 0, sizeof(o));
+#define CASE(MM)                                                                                 \
+    case MM:                                                                                       \
+        if (ns == 0) run_caps<MM, 0>(caps, prop, sids, src, duration_ms, o);                      \
+        else if (ns == 1) run_caps<MM, 1>(caps, prop, sids, src, duration_ms, o);                 \
+        else if (ns == 2) run_caps<MM, 2>(caps, prop, sids, src, duration_ms, o);                 \
+        else run_caps<MM, 4>(caps, prop, sids, src, duration_ms, o);                              \
+        break;
+    switch (m) { MSIM_FOR_EACH_M(CASE) default: return -1; }
+#undef CASE
+    for (int k = 0; k < m; ++k) {
+        found[k] = o.found[k];
+        stale[k] = o.stale[k];
+    }
+    *best_height = o.best_height;
+    *err = o.err;
+    return 0;
+}

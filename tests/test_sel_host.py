@@ -1,0 +1,183 @@
+"""The product's entity engine (miningsimulation_amd/csrc/msim_sel.h), built for the host
+(tests/native/sel_host.cpp, test-only), against the oracle: per-run found and stale counters and the
+best-chain height must be identical (bit-exact integer parity).
+
+Covers what the device's selfish path runs (BASELINE configs[2], configs[3]) and what the reference allows
+beyond it: several selfish miners (simulation.h:55 is a per-miner flag), selfish miners at any index,
+heterogeneous propagation, integer weights, honest networks, and the capacity error
+paths. tests/test_gpu_selfish.py checks the gfx950 build of the same header against the same oracle."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+D = 31_556_952_000
+
+
+@pytest.fixture(scope="module")
+def sel(native_tests):
+    lib = ctypes.CDLL(native_tests["sel_host"])
+    lib.sel_run.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                            ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_uint64, ctypes.c_int64,
+                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
+                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                            ctypes.POINTER(ctypes.c_uint32)]
+
+    def run(weights, props, selfish, duration, si, sp, caps=0, W=100):
+        m = len(weights)
+        f = (ctypes.c_uint32 * m)()
+        s = (ctypes.c_uint32 * m)()
+        bh = ctypes.c_uint32()
+        err = ctypes.c_uint32()
+        rc = lib.sel_run((ctypes.c_uint64 * m)(*weights), (ctypes.c_int64 * m)(*props),
+                         (ctypes.c_uint8 * m)(*[1 if x else 0 for x in selfish]), m, W, duration, si, sp, caps, f, s,
+                         ctypes.byref(bh), ctypes.byref(err))
+        assert rc == 0
+        return err.value, np.array([[f[k], s[k]] for k in range(m)], dtype=np.int64), bh.value
+
+    return run
+
+
+def _rand_percs(m, rng, total=100):
+    cuts = sorted(rng.sample(range(1, total), m - 1)) if m > 1 else []
+    b = [0] + cuts + [total]
+    return [b[i + 1] - b[i] for i in range(m)]
+
+
+def _oracle(oracle, weights, props, selfish, duration, si, sp, W=100):
+    if W == 100:
+        rc, res, bh = oracle.run(weights, props, selfish, duration, si, sp)
+        assert rc == 0
+        return res, bh
+    # weighted networks: one run through the batch API (run r = 0 uses seeds (base, base + 1))
+    assert sp == si + 1
+    f, s, _, _ = oracle.run_batch(weights, props, selfish, duration, 1, 0, si, threads=1, total_weight=W)
+    return np.stack([f[0], s[0]], axis=1), int(f[0].sum())
+
+
+def _check(sel, oracle, weights, props, selfish, duration, si, sp, caps=0, W=100, allow_err=False):
+    ores, obh = _oracle(oracle, weights, props, selfish, duration, si, sp, W)
+    err, mres, mbh = sel(weights, props, selfish, duration, si, sp, caps, W)
+    if allow_err and err:
+        return err
+    assert err == 0, f"capacity error {err} for {weights} {props} {selfish} {duration} {si} {sp}"
+    assert np.array_equal(ores, mres), (weights, props, selfish, duration, si, sp, ores.tolist(), mres.tolist())
+    if W == 100:
+        assert obh == mbh, (obh, mbh)
+    return 0
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_networks(sel, oracle, seed):
+    rng = random.Random(4321 + seed)
+    for _ in range(40):
+        m = rng.randint(1, 15)
+        percs = _rand_percs(m, rng)
+        if rng.random() < 0.3:
+            props = [rng.choice([0, 1, 50, 100, 1000, 10_000, 30_000, 60_000]) for _ in range(m)]
+        else:
+            props = [rng.choice([100, 1000, 10_000, 30_000])] * m
+        s = rng.randrange(m) if (m > 1 and rng.random() < 0.6) else -1
+        selfish = [k == s for k in range(m)]
+        duration = rng.choice([10**7, 10**8, 10**9])
+        _check(sel, oracle, percs, props, selfish, duration, rng.randrange(2**32), rng.randrange(2**32), caps=1)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_multiple_selfish(sel, oracle, seed):
+    """Two to four selfish miners in one network (the reference's is_selfish is per miner). Every run is
+    bit-exact or flagged; only networks whose selfish miners hold most of the hashrate (three long branches
+    at once) may exceed the two deep branches of the window."""
+    rng = random.Random(777 + seed)
+    flagged = 0
+    for _ in range(25):
+        m = rng.randint(2, 12)
+        percs = _rand_percs(m, rng)
+        ns = rng.randint(2, min(4, m))
+        sidx = set(rng.sample(range(m), ns))
+        selfish = [k in sidx for k in range(m)]
+        if rng.random() < 0.5:
+            props = [rng.choice([0, 100, 1000, 10_000, 30_000]) for _ in range(m)]
+        else:
+            props = [rng.choice([100, 1000, 10_000])] * m
+        duration = rng.choice([10**8, 10**9, 3 * 10**9])
+        majority = sum(p for p, s in zip(percs, selfish) if s) > 50
+        if _check(sel, oracle, percs, props, selfish, duration, rng.randrange(2**32), rng.randrange(2**32), caps=1,
+                  allow_err=majority):
+            flagged += 1
+    assert flagged <= 3
+
+
+@pytest.mark.parametrize("h,prop", [(40, 1000), (49, 30_000), (45, 10_000), (25, 100), (10, 30_000), (49, 100),
+                                    (30, 5000)])
+def test_selfish_full_year(sel, oracle, h, prop):
+    """configs[2] and corners of the configs[3] grid, full year, with the fast kernel's capacities:
+    anything they cannot hold must be flagged (never wrong), and the retry capacities must be exact."""
+    percs = [h, 59 - h, 12, 11, 8, 5, 3, 1, 1]
+    for r in range(2):
+        si, sp = 1000 + 2 * r, 1001 + 2 * r
+        if _check(sel, oracle, percs, [prop] * 9, [True] + [False] * 8, D, si, sp, caps=0, allow_err=True):
+            _check(sel, oracle, percs, [prop] * 9, [True] + [False] * 8, D, si, sp, caps=1)
+
+
+@pytest.mark.parametrize("prop", [100, 10_000])
+def test_honest_full_year_presets(sel, oracle, prop):
+    for r in range(2):
+        _check(sel, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [prop] * 9, [False] * 9, D, 1000 + 2 * r, 1001 + 2 * r,
+               caps=1)
+
+
+def test_fast_capacities_flag_or_match(sel, oracle):
+    """With the smallest capacities every run is either bit-exact or flagged."""
+    rng = random.Random(5)
+    flagged = 0
+    for _ in range(60):
+        m = rng.randint(2, 9)
+        percs = _rand_percs(m, rng)
+        props = [rng.choice([1000, 30_000, 120_000])] * m
+        s = rng.randrange(m)
+        selfish = [k == s for k in range(m)]
+        flagged += bool(_check(sel, oracle, percs, props, selfish, 10**9, rng.randrange(2**32), rng.randrange(2**32),
+                               caps=2, allow_err=True))
+    assert flagged > 0  # the tiny capacities must actually be exceeded somewhere
+
+
+def test_huge_delays(sel, oracle):
+    rng = random.Random(99)
+    for _ in range(15):
+        m = rng.randint(2, 9)
+        percs = _rand_percs(m, rng)
+        props = [rng.choice([60_000, 120_000, 300_000]) for _ in range(m)]
+        s = rng.randrange(m) if rng.random() < 0.5 else -1
+        selfish = [k == s for k in range(m)]
+        _check(sel, oracle, percs, props, selfish, 10**9, rng.randrange(2**32), rng.randrange(2**32), caps=1,
+               allow_err=True)
+
+
+def test_weighted_networks(sel, oracle):
+    """Integer weights summing to W != 100, with selfish miners."""
+    rng = random.Random(31)
+    for _ in range(12):
+        m = rng.randint(2, 10)
+        W = rng.choice([17, 1000, 102_400, 2**20 + 3])
+        w = _rand_percs(m, rng, W)
+        s = rng.randrange(m)
+        selfish = [k == s for k in range(m)]
+        props = [rng.choice([100, 1000, 10_000])] * m
+        si = rng.randrange(2**31)
+        _check(sel, oracle, w, props, selfish, 10**9, si, si + 1, caps=1, W=W)
+
+
+def test_edge_cases(sel, oracle):
+    # one miner, zero propagation, zero/one-ms durations, a 0% miner, selfish first/last, all-selfish
+    _check(sel, oracle, [100], [0], [False], 10**9, 5, 6)
+    _check(sel, oracle, [100], [500], [True], 10**9, 5, 6)
+    _check(sel, oracle, [50, 50], [0, 0], [False, False], 10**9, 7, 8)
+    _check(sel, oracle, [60, 40], [0, 0], [True, False], 10**9, 7, 8)
+    _check(sel, oracle, [40, 60], [0, 0], [False, True], 10**9, 7, 8)
+    _check(sel, oracle, [50, 50], [0, 1000], [True, True], 10**9, 7, 8, caps=1)
+    _check(sel, oracle, [30, 0, 70], [1000, 1000, 1000], [False, True, False], 10**9, 9, 10)
+    _check(sel, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, 0, 1, 2)
+    _check(sel, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, 1, 1, 2)
+    _check(sel, oracle, [10, 20, 30, 40], [1000] * 4, [False, False, False, True], 10**9, 11, 12)
