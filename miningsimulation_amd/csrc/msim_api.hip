@@ -310,7 +310,8 @@ uint32_t word_draw_slots()
 struct SelWs {
     msim::SelLayout L;
     uint32_t wpp, err_cap;
-    size_t counts_off, partials_off, retry_off, list_off, words_off, total;
+    size_t cold_lanes;
+    size_t counts_off, partials_off, retry_off, list_off, cold_off, words_off, total;
 };
 
 SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
@@ -325,7 +326,12 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
     w.partials_off = 256;
     w.retry_off = al(w.partials_off + (size_t)np * w.wpp * nv * 8);
     w.list_off = al(w.retry_off + (size_t)np * nv * 8);
-    w.words_off = al(w.list_off + (size_t)w.err_cap * 4);
+    // cold slots: one set per E1 lane of a slice (every point x the slice's runs, rounded to whole
+    // workgroups) and per E2 lane
+    const size_t e1 = (size_t)np * ((w.L.nr + msim::TPB - 1) / msim::TPB) * msim::TPB;
+    w.cold_lanes = e1 > w.err_cap ? e1 : (size_t)w.err_cap;
+    w.cold_off = al(w.list_off + (size_t)w.err_cap * 4);
+    w.words_off = al(w.cold_off + w.cold_lanes * msim::SEL_NC * sizeof(msim::ColdAct));
     w.total = al(w.words_off + w.L.words_bytes);
     return w;
 }
@@ -347,21 +353,11 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
         sp->prop[k] = miners[k].propagation_ms;
         if (miners[k].is_selfish) sp->sids[sp->ns++] = k;
     }
-    // word code -> finder: W = 100 words carry q = floor(u / PERC_MULTIPLIER) (first k with cum_k > q,
-    // simulation.h:217-218); weighted words carry the finder itself.
-    for (uint32_t q = 0; q < SEL_LUT; ++q) {
-        uint32_t f = 15;
-        if (W == 100) {
-            for (uint32_t k = 0; k < n && q <= 100; ++k)
-                if (sp->cum[k] > q) {
-                    f = k;
-                    break;
-                }
-        } else if (q < n) {
-            f = q;
-        }
-        sp->lut[q] = (uint8_t)f;
-    }
+    for (int k = 0; k < MAXM; ++k)
+        sp->ccum[k] = (uint32_t)k < n ? (W == 100 ? (uint32_t)sp->cum[k] : (uint32_t)k + 1u) : 0xFFFFFFFFu;
+    sp->uniform_prop = 1;
+    for (uint32_t k = 1; k < n; ++k)
+        if (miners[k].propagation_ms != miners[0].propagation_ms) sp->uniform_prop = 0;
 }
 
 struct SelGroupDev {
@@ -398,6 +394,8 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     a.err_list = (uint32_t *)(ws + w.list_off);
     a.err_cap = w.err_cap;
     a.force_retry = getenv("MSIM_SEL_FORCE_RETRY") != nullptr ? 1u : 0u;
+    a.cold = (ColdAct *)(ws + w.cold_off);
+    a.cold_lanes = w.cold_lanes;
     WordArgs da = wt;
     da.seed_base = seed_base;
     da.nr = w.L.nr;

@@ -11,27 +11,10 @@
 #include <hip/hip_runtime.h>
 
 #include "msim_kernels.h"
+#include "msim_reduce.h"
 #include "msim_pipeline.h"
-#include "msim_sel_launch.h"
 
 namespace msim {
-
-// Wave-level (DPP/bpermute) reduction of 6*M 64-bit sums, then the workgroup's 4 waves through LDS.
-template <int M>
-__device__ __forceinline__ void block_reduce_store(const uint64_t (&v)[6 * M], uint64_t *__restrict__ out)
-{
-    __shared__ uint64_t red[TPB / 64][6 * M];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = 0; i < 6 * M; ++i) {
-        unsigned long long x = v[i];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        if (lane == 0) red[wv][i] = x;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 6 * M; i += TPB) out[i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-}
 
 template <int M, bool SELF, bool DEEP, int NX, int NG, bool LIST>
 __global__ __launch_bounds__(TPB, 2) void msim_runs_kernel(const SimParams p, const uint64_t run_begin, const uint32_t n,
@@ -362,234 +345,12 @@ static hipError_t launch_sweep_impl(const SweepArgs &a)
     return launch_sweep_finalize(a);
 }
 
-// ------------------------------------------------------------------ entity engine (msim_sel.h)
-// Per-lane counters of the engine in LDS, [array][miner][lane]: lanes of a wave hit distinct banks for any
-// mix of miner indices.
-template <int M>
-struct SelDevEnv {
-    uint32_t *c;          // &s_cnt[0][tid]
-    const int64_t *pr;    // propagation per miner (LDS or global)
-    __device__ __forceinline__ int64_t prop(uint32_t k) const { return pr[k]; }
-    __device__ __forceinline__ uint32_t get(int a, uint32_t k) const { return c[(a * M + (int)k) * TPB]; }
-    __device__ __forceinline__ void add(int a, uint32_t k, uint32_t v) { c[(a * M + (int)k) * TPB] += v; }
-    __device__ __forceinline__ void set(int a, uint32_t k, uint32_t v) { c[(a * M + (int)k) * TPB] = v; }
-};
-
-// The run's words (msim_sel_launch.h D1 layout), four at a time, the next four already in flight.
-struct SelWordSrc {
-    const uint4 *p;  // uint4 (row, run) base of this run
-    size_t row;      // uint4 per tile row = nr * 8
-    uint32_t b, nb;
-    uint32_t c0, c1, c2, c3;  // current four words, consumed by shifting (no indexed pick)
-    uint4 nxt;
-    const uint8_t *lut;
-    __device__ __forceinline__ uint4 ld(uint32_t c) const { return p[(size_t)(c / SEL_TILE) * row + ((c % SEL_TILE) >> 2)]; }
-    __device__ __forceinline__ void init()
-    {
-        b = 0;
-        const uint4 x = ld(0);
-        c0 = x.x;
-        c1 = x.y;
-        c2 = x.z;
-        c3 = x.w;
-        nxt = ld(4);
-    }
-    __device__ __forceinline__ bool next(uint32_t &I, uint32_t &k)
-    {
-        if (b >= nb) return false;
-        const uint32_t w = c0;
-        c0 = c1;
-        c1 = c2;
-        c2 = c3;
-        ++b;
-        if ((b & 3u) == 0) {
-            c0 = nxt.x;
-            c1 = nxt.y;
-            c2 = nxt.z;
-            c3 = nxt.w;
-            if (b + 4 < nb) nxt = ld(b + 4);
-        }
-        I = w >> 7;
-        k = lut[w & 127u];
-        return true;
-    }
-};
-
-// The reference's draws recomputed in-lane (retry): exact NextBlockInterval and PickFinder with
-// integer weights (q = floor(u / MULT) is p1 = floor(W u / 2^64) or p1 + 1; first k with cum_k > q).
-struct SelRngSrc {
-    Rng ri, rp;
-    const SelParams *P;
-    __device__ bool next(uint32_t &I, uint32_t &k)
-    {
-        I = (uint32_t)next_interval(ri);
-        const uint64_t u = rng_next(rp);
-        const uint64_t p1 = __umul64hi(u, (uint64_t)P->W);
-        const uint64_t q = u >= (p1 + 1) * P->mult ? p1 + 1 : p1;
-        uint32_t f = 0;
-        for (uint32_t j = 0; j < P->m; ++j) f += P->cum[j] <= q ? 1u : 0u;
-        k = f;
-        return true;
-    }
-};
-
-template <int M>
-__device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
-{
-    const double L = (double)o.best_height;
-#pragma unroll
-    for (int k = 0; k < M; ++k) {
-        const uint32_t f = o.found[k];
-        // MinerStats (main.cpp:28-29)
-        const double share = f == 0 ? 0.0 : (double)f / L;
-        const double rate = f == 0 ? 0.0 : (double)o.stale[k] / (double)f;
-        const uint64_t sfx = (uint64_t)(share * 4294967296.0 + 0.5);
-        const uint64_t rfx = (uint64_t)(rate * 4294967296.0 + 0.5);
-        v[6 * k + 0] = f;
-        v[6 * k + 1] = o.stale[k];
-        v[6 * k + 2] = sfx >> 32;
-        v[6 * k + 3] = sfx & 0xFFFFFFFFull;
-        v[6 * k + 4] = rfx >> 32;
-        v[6 * k + 5] = rfx & 0xFFFFFFFFull;
-    }
-}
-
-// E1: one lane per (point, run of the slice); workgroups never straddle points.
-template <int M, int NS, int NA, int NG, int NQ>
-__global__ __launch_bounds__(TPB) void msim_sel_kernel(const SelArgs a)
-{
-    __shared__ uint32_t s_cnt[4 * M][TPB];
-    __shared__ int64_t s_prop[MAXM];
-    __shared__ uint8_t s_lut[SEL_LUT];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t wps = (a.sn + TPB - 1) / TPB;
-    const uint32_t point = a.plist[blockIdx.x / wps], blk = blockIdx.x % wps;
-    const SelParams *P = a.pts + point;
-    if (tid < MAXM) s_prop[tid] = P->prop[tid];
-    if (tid < SEL_LUT) s_lut[tid] = P->lut[tid];
-#pragma unroll
-    for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
-    __syncthreads();
-    const uint32_t lr = blk * TPB + tid;
-    const bool active = lr < a.sn;
-    const uint32_t rel = a.s0 + lr;
-    uint64_t v[6 * M];
-#pragma unroll
-    for (int i = 0; i < 6 * M; ++i) v[i] = 0;
-    if (active) {
-        SelDevEnv<M> env{&s_cnt[0][tid], s_prop};
-        SelWordSrc src;
-        src.p = reinterpret_cast<const uint4 *>(a.words) + (size_t)lr * (SEL_TILE / 4);
-        src.row = (size_t)a.nr * (SEL_TILE / 4);
-        src.nb = a.nb;
-        src.lut = s_lut;
-        src.init();
-        Sel<M, NS, NA, NG, NQ> s;
-        s.init(P->m, P->sids);
-        SelOut o;
-        if (a.force_retry) o.err = SERR_CAP;
-        else s.run(env, src, P->duration_ms, o);
-        if (o.err) {
-            const uint32_t pos = atomicAdd(a.counts, 1u);
-            if (pos < a.err_cap) a.err_list[pos] = point * a.rpp + rel;
-        } else {
-            sel_terms<M>(o, v);
-            const size_t g = (size_t)point * a.rpp + rel;
-            if (a.records)
-#pragma unroll
-                for (int k = 0; k < M; ++k) {
-                    a.records[2 * (g * M + k) + 0] = o.found[k];
-                    a.records[2 * (g * M + k) + 1] = o.stale[k];
-                }
-            if (a.best_h) a.best_h[g] = o.best_height;
-        }
-    }
-    block_reduce_store<M>(v, a.partials + ((size_t)point * a.wpp + a.s0 / TPB + blk) * 6 * M);
-}
-
-// E2: one lane per flagged (point, run), wide capacities, draws from the seeds.
-template <int M, int NS>
-__global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
-{
-    __shared__ uint32_t s_cnt[4 * M][TPB];
-    const uint32_t tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
-    const uint32_t c = *a.counts, lim = c < a.err_cap ? c : a.err_cap;
-    const uint32_t idx = blockIdx.x * TPB + tid;
-    if (idx >= lim) return;
-    const uint32_t code = a.err_list[idx];
-    const uint32_t point = code / a.rpp, rel = code % a.rpp;
-    const SelParams *P = a.pts + point;
-    const uint64_t run = a.run_begin + rel;
-    SelDevEnv<M> env{&s_cnt[0][tid], P->prop};
-    SelRngSrc src{rng_seed(seed_interval(a.seed_base, run)), rng_seed(seed_picker(a.seed_base, run)), P};
-    Sel<M, NS, 8, 16, 8> s;
-    s.init(P->m, P->sids);
-    SelOut o;
-    s.run(env, src, P->duration_ms, o);
-    if (o.err) {
-        atomicAdd(a.counts + 1, 1u);
-        return;
-    }
-    uint64_t v[6 * M];
-    sel_terms<M>(o, v);
-    const size_t g = (size_t)point * a.rpp + rel;
-    if (a.records)
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-            a.records[2 * (g * M + k) + 0] = o.found[k];
-            a.records[2 * (g * M + k) + 1] = o.stale[k];
-        }
-    if (a.best_h) a.best_h[g] = o.best_height;
-#pragma unroll
-    for (int i = 0; i < 6 * M; ++i)
-        if (v[i]) atomicAdd((unsigned long long *)(a.retry_sums + (size_t)point * 6 * M + i), (unsigned long long)v[i]);
-}
-
-template <int M, int NS>
-static hipError_t launch_sel_ns(const SelArgs &a, uint32_t caps, hipStream_t s)
-{
-    const uint32_t wps = (a.sn + TPB - 1) / TPB;
-    const dim3 grid(a.nlist * wps);
-    if (caps == SEL_SMALL)
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2>), grid, dim3(TPB), 0, s, a);
-    else
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 4, 8, 3>), grid, dim3(TPB), 0, s, a);
-    return hipGetLastError();
-}
-
 #if defined(MSIM_M)
 // One translation unit per miner count (built in parallel): explicit entry point for M = MSIM_M.
 #define MSIM_CAT2(a, b) a##b
 #define MSIM_CAT(a, b) MSIM_CAT2(a, b)
 hipError_t MSIM_CAT(launch_runs_m, MSIM_M)(const LaunchArgs &a) { return launch_m<MSIM_M>(a); }
 hipError_t MSIM_CAT(launch_sweep_m, MSIM_M)(const SweepArgs &a) { return launch_sweep_impl<MSIM_M>(a); }
-hipError_t MSIM_CAT(launch_sel_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, uint32_t caps, hipStream_t s)
-{
-    if (ns_class == 1) return launch_sel_ns<MSIM_M, 1>(a, caps, s);
-#if MSIM_M >= 2
-    // several selfish miners: the wide capacities in E1 as well
-    const uint32_t wps = (a.sn + TPB - 1) / TPB;
-    if (ns_class == 2)
-        hipLaunchKernelGGL((msim_sel_kernel<MSIM_M, 2, 4, 8, 3>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-    else
-        hipLaunchKernelGGL((msim_sel_kernel<MSIM_M, 4, 4, 8, 3>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-    return hipGetLastError();
-#else
-    return hipErrorInvalidValue;
-#endif
-}
-hipError_t MSIM_CAT(launch_sel_retry_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, hipStream_t s)
-{
-    const dim3 grid((a.err_cap + TPB - 1) / TPB);
-    if (ns_class == 1) hipLaunchKernelGGL((msim_sel_retry_kernel<MSIM_M, 1>), grid, dim3(TPB), 0, s, a);
-#if MSIM_M >= 2
-    else if (ns_class == 2) hipLaunchKernelGGL((msim_sel_retry_kernel<MSIM_M, 2>), grid, dim3(TPB), 0, s, a);
-    else hipLaunchKernelGGL((msim_sel_retry_kernel<MSIM_M, 4>), grid, dim3(TPB), 0, s, a);
-#endif
-    return hipGetLastError();
-}
 #endif
 
 }  // namespace msim

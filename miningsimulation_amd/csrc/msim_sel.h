@@ -24,20 +24,35 @@
 // 16-height window of 4-bit owners per entity above settled per-owner counters, two deep-branch counter
 // sets for long selfish episodes, and an implicit single-owner run above the window (a selfish miner's
 // withheld run, or anything that adopted it). Per-owner counters live in the Env (LDS on the device).
-// Capacities (active slots, reveal groups, in-flight blocks, window) only ever set an error bit; the
-// caller recomputes such runs with larger capacities, so results never depend on them.
+//
+// Hot and cold slots. P, the selfish entities and NA active slots live in registers. A miner that
+// becomes active when the NA slots are taken, or whose in-flight queue outgrows NQ, moves to one of NC
+// COLD slots kept in the Env (global memory on the device) with a deeper queue. Cold slots are touched
+// only when some lane of a wave has one (measured: the second active slot is needed in 8-11 % of wave
+// iterations at 1 s, a third far less), so the common path stays short and register-resident while a run
+// practically never exceeds a capacity. Anything that does (all cold slots taken, a window that cannot
+// fold) sets an error bit and the run is recomputed with wider capacities: results never depend on them.
 #pragma once
 #include "msim_model.h"
+
+// Region markers for the host SIMT probe (tests/native); no code in product builds.
+#ifndef SEL_HIT
+#define SEL_HIT(region)
+#endif
 
 namespace msim {
 
 constexpr uint32_t SEL_NONE = 0xFu;  // "no owner" (miner ids are < 15)
 constexpr int SEL_MAXS = 4;          // selfish miners per network supported by the entity engine
+constexpr int SEL_NQC = 6;           // in-flight blocks of a cold active slot
 enum : uint32_t {
-    SERR_CAP = 1u,    // active slots / reveal groups / in-flight queue exhausted
-    SERR_WIN = 2u,    // a chain outgrew the window and could not fold
-    SERR_PICK = 4u,   // PickFinder fell through (simulation.h:220 assert)
-    SERR_DRAWS = 8u,  // the run outlasted its pre-generated draws
+    SERR_WIN = 2u,     // a chain outgrew the window and could not fold
+    SERR_PICK = 4u,    // PickFinder fell through (simulation.h:220 assert)
+    SERR_DRAWS = 8u,   // the run outlasted its pre-generated draws
+    SERR_ACT = 16u,    // active slots (hot and cold) exhausted
+    SERR_GRP = 32u,    // reveal groups exhausted
+    SERR_QUE = 64u,    // in-flight queue of a cold active slot exhausted
+    SERR_CAP = SERR_ACT | SERR_GRP | SERR_QUE,
 };
 // Counter arrays of the Env: settled found, stale_blocks, deep branch A, deep branch B.
 enum : int { C_F = 0, C_S = 1, C_A = 2, C_B = 3 };
@@ -49,61 +64,134 @@ struct SelOut {
     uint32_t err;
 };
 
-// The best chain of one event: entity, published tip height, tip arrival, window string (owners above
-// the tip = 0xF), implicit run owner (heights >= WIN), deep branch.
+// One chain: owners at window heights wb..wb+15 (0xF above the tip), tip and published tip heights
+// relative to wb (heights WIN..rt are owned by xo, the implicit run), arrival of the published tip
+// (BestChain's first-seen key, main.cpp:75), deep branch (0 = A, 1 = B).
+struct Ent {
+    uint64_t s;
+    int32_t rt, rp;
+    int64_t pa;
+    uint32_t xo, br;
+};
+
+// A cold active slot (Env storage).
+struct ColdAct {
+    Ent x;
+    uint32_t aid;  // its miner
+    int32_t nq;
+    int64_t q[SEL_NQC];  // own in-flight blocks, lowest first
+};
+
+// The best chain of one event: published tip height, tip arrival, window string truncated at the tip,
+// implicit run owner (heights >= WIN), deep branch.
 struct SelBest {
-    int e;
     int32_t l;
     int64_t a;
     uint64_t s;
-    uint32_t x;
-    uint32_t br;
+    uint32_t x, br;
 };
 
+MSIM_HD void ent_reset(Ent &x)
+{
+    x.s = ~0ull;
+    x.rt = -1;  // genesis (height 0) is settled: wb = 1
+    x.rp = -1;
+    x.pa = 0;   // Genesis arrival (simulation.h:31-33)
+    x.xo = SEL_NONE;
+    x.br = 0;
+}
+
+// Room for a block of owner o at height rt + 1: inside the window, the first implicit-run height, or an
+// implicit run of the same owner.
+MSIM_HD bool ent_room(const Ent &x, uint32_t o) { return x.rt + 1 <= WIN || x.xo == o; }
+
+MSIM_HD void ent_append(Ent &x, uint32_t o)
+{
+    const int h = x.rt + 1;
+    if (h < WIN) x.s = (x.s & ~(0xFull << (4 * h))) | ((uint64_t)o << (4 * h));
+    else if (h == WIN) x.xo = o;
+    x.rt = h;
+}
+
+MSIM_HD void ent_shift(Ent &x, int s, uint64_t fill)
+{
+    x.s = (x.s >> (4 * s)) | fill;
+    x.rt -= s;
+    x.rp -= s;
+    if (x.rt >= WIN - s && x.xo != SEL_NONE) {  // heights entering the window from the implicit run
+        const uint64_t mk = nib_range(WIN - s, imin(x.rt, WIN - 1));
+        x.s = (x.s & ~mk) | (mk & (0x1111111111111111ull * (uint64_t)x.xo));
+    }
+    if (x.rt < WIN) x.xo = SEL_NONE;
+}
+
+// c ? a : b field by field. A conditional whole-struct copy would become a copy through a selected
+// pointer, which keeps both structs out of registers.
+MSIM_HD Ent ent_pick(bool c, const Ent &a, const Ent &b)
+{
+    Ent r;
+    r.s = c ? a.s : b.s;
+    r.rt = c ? a.rt : b.rt;
+    r.rp = c ? a.rp : b.rp;
+    r.pa = c ? a.pa : b.pa;
+    r.xo = c ? a.xo : b.xo;
+    r.br = c ? a.br : b.br;
+    return r;
+}
+
+// An active miner whose chain is the class's chain again, all published, rejoins the class.
+MSIM_HD bool ent_same_as_p(const Ent &x, const Ent &P)
+{
+    return x.rp == x.rt && x.rt == P.rt && x.s == P.s && x.xo == P.xo && x.br == P.br;
+}
+
 // Env: int64_t prop(uint32_t k); uint32_t get(int arr, uint32_t k); void add(int arr, uint32_t k, uint32_t v);
-//      void set(int arr, uint32_t k, uint32_t v).
+//      void set(int arr, uint32_t k, uint32_t v); ColdAct cold(int c); void cold_put(int c, const ColdAct &).
 // Src: bool next(uint32_t &interval_ms, uint32_t &finder)  (finder >= M: PickFinder fell through).
-template <int M, int NS, int NA, int NG, int NQ>
+template <int M, int NS, int NA, int NG, int NQ, int NC>
 struct Sel {
     static_assert(M >= 1 && M <= MAXM, "miner count");
-    static_assert(NS >= 0 && NS <= SEL_MAXS && NA >= 1 && NG >= 1 && NQ >= 1, "capacities");
+    static_assert(NS >= 0 && NS <= SEL_MAXS && NA >= 1 && NG >= 1 && NQ >= 1 && NC >= 0 && NC <= 7, "capacities");
     static constexpr int NSA = NS > 0 ? NS : 1;
-    static constexpr int E0A = 1 + NS;  // first active entity
-    static constexpr int NE = 1 + NS + NA;
 
-    uint64_t str[NE];  // owners at window heights wb..wb+15 (0xF above the tip)
-    int32_t rt[NE];    // tip height - wb (>= WIN: heights WIN..rt are owned by xo)
-    int32_t rp[NE];    // published tip height - wb (PublishedChain, simulation.h:118-121)
-    int64_t pa[NE];    // arrival of the published tip (BestChain's first-seen key, main.cpp:75)
-    uint32_t xo[NE];   // owner of the implicit run above the window (SEL_NONE when rt < WIN)
-    uint32_t vm;       // valid entities
-    uint32_t bm;       // deep branch of each entity (bit e set: branch B)
+    Ent P;
+    Ent S[NSA];
+    Ent A[NA];
     uint32_t sidv[NSA];
     int32_t w[NSA];    // withheld blocks (SelfishBlocks)
     int32_t ng[NSA];   // in-flight reveal groups, oldest first
     int32_t gc[NSA][NG];
     int64_t ga[NSA][NG];
-    uint32_t aid[NA];  // miner of each active slot (SEL_NONE = free)
+    uint32_t aid[NA];  // miner of each hot active slot
     int32_t nq[NA];    // own in-flight blocks, lowest first (only own blocks are ever unpublished)
     int64_t q[NA][NQ];
+    uint32_t sv, av, cm;  // valid selfish entities / hot active slots / occupied cold slots
+    uint32_t caid;     // miner of each cold slot, 4 bits per slot
     uint32_t am, hm, sm;  // active / honest / selfish miner masks
     uint32_t wb;       // absolute height of window position 0
     int32_t bpub;      // previous event's best tip - wb (best_chain_size - 1, main.cpp:171)
     bool deep;
     uint32_t err;
 
-    MSIM_HD bool valid(int e) const { return (vm >> e) & 1u; }
-    MSIM_HD uint32_t ebr(int e) const { return (bm >> e) & 1u; }
-    MSIM_HD uint32_t owner(int e) const { return e == 0 ? SEL_NONE : (e < E0A ? sidv[e - 1] : aid[e - E0A]); }
+    MSIM_HD bool sval(int si) const { return (sv >> si) & 1u; }
+    MSIM_HD bool aval(int a) const { return (av >> a) & 1u; }
+    MSIM_HD bool cval(int c) const { return (cm >> c) & 1u; }
+    MSIM_HD uint32_t cold_aid(int c) const { return (caid >> (4 * c)) & 15u; }
 
     // sids: NSA selfish miner ids in index order (SEL_NONE for unused entries); m miners.
     MSIM_HD void init(uint32_t m, const uint32_t *sids)
     {
         sm = 0;
+        sv = 0;
+        ent_reset(P);
 #pragma unroll
         for (int si = 0; si < NSA; ++si) {
             sidv[si] = NS > 0 ? sids[si] : SEL_NONE;
-            if (sidv[si] != SEL_NONE) sm |= 1u << sidv[si];
+            if (sidv[si] != SEL_NONE) {
+                sm |= 1u << sidv[si];
+                sv |= 1u << si;
+            }
+            ent_reset(S[si]);
             w[si] = 0;
             ng[si] = 0;
 #pragma unroll
@@ -113,25 +201,18 @@ struct Sel {
             }
         }
         hm = ((1u << m) - 1u) & ~sm;
-        vm = 1u;
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            str[e] = ~0ull;
-            rt[e] = -1;  // genesis (height 0) is settled: wb = 1
-            rp[e] = -1;
-            pa[e] = 0;   // Genesis arrival (simulation.h:31-33)
-            xo[e] = SEL_NONE;
-            if (e >= 1 && e < E0A && sidv[e - 1] != SEL_NONE) vm |= 1u << e;
-        }
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
+            ent_reset(A[a]);
             aid[a] = SEL_NONE;
             nq[a] = 0;
 #pragma unroll
             for (int i = 0; i < NQ; ++i) q[a][i] = T_INF;
         }
+        av = 0;
+        cm = 0;
+        caid = 0;
         am = 0;
-        bm = 0;
         wb = 1;
         bpub = -1;  // best_chain_size = 1 (main.cpp:149)
         deep = false;
@@ -141,7 +222,7 @@ struct Sel {
     MSIM_HD void push_group(int si, int32_t c, int64_t arr)
     {
         if (ng[si] >= NG) {
-            err |= SERR_CAP;
+            err |= SERR_GRP;
             return;
         }
         // unconditional selects: a predicated store per slot would become a store through a selected
@@ -154,15 +235,160 @@ struct Sel {
         }
         ng[si]++;
     }
-    MSIM_HD void enqueue(int a, int64_t arr)
+
+    // ------------------------------------------------------------------ cold slots
+    MSIM_HD int free_cold() const
     {
-        if (nq[a] >= NQ) {
-            err |= SERR_CAP;
+        int c = -1;
+#pragma unroll
+        for (int i = NC - 1; i >= 0; --i)
+            if (!cval(i)) c = i;
+        return c;
+    }
+    MSIM_HD void take_cold(int c, uint32_t k)
+    {
+        cm |= 1u << c;
+        caid = (caid & ~(15u << (4 * c))) | (k << (4 * c));
+    }
+
+    // ------------------------------------------------------------------ Miner::FoundBlock
+    // simulation.h:62-76 for miner k at time T. A passive miner leaves the class with its chain.
+    template <class Env>
+    MSIM_HD void found(Env &env, uint32_t k, int64_t T)
+    {
+        const int64_t arr = T + env.prop(k);
+        if ((sm >> k) & 1u) {
+            SEL_HIT(1);
+#pragma unroll
+            for (int si = 0; si < NS; ++si) {
+                if (sidv[si] != k) continue;
+                if (!ent_room(S[si], k)) {
+                    err |= SERR_WIN;
+                    return;
+                }
+                const bool race = (w[si] == 1) && (bpub == S[si].rt);  // simulation.h:66
+                if (race) {
+                    w[si] = 0;
+                    push_group(si, 2, arr);  // simulation.h:68-69: both blocks arrive at T + prop
+                } else {
+                    w[si] += 1;  // simulation.h:71 (SELFISH_ARRIVAL)
+                }
+                ent_append(S[si], k);
+            }
             return;
         }
+        // An honest miner: its hot slot, a free hot slot (leaving the class), or the cold path.
+        int at = -1;
+        const bool was_active = (am >> k) & 1u;
+        if (was_active) {
+            SEL_HIT(2);
 #pragma unroll
-        for (int i = 0; i < NQ; ++i) q[a][i] = (i == nq[a]) ? arr : q[a][i];
-        nq[a]++;
+            for (int a = 0; a < NA; ++a)
+                if (aval(a) && aid[a] == k) at = a;
+        } else {
+            SEL_HIT(3);
+#pragma unroll
+            for (int a = NA - 1; a >= 0; --a)
+                if (!aval(a)) at = a;
+        }
+        bool hot = at >= 0;
+        int32_t qn = 0;
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+            if (a == at) qn = was_active ? nq[a] : 0;
+        if (hot && qn >= NQ) hot = false;  // a hot slot whose queue is full moves to a cold slot
+        if (hot) {
+            // selects over the slots (see push_group)
+            Ent x = P;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) x = ent_pick(a == at && was_active, A[a], x);
+            if (!ent_room(x, k)) {
+                err |= SERR_WIN;
+                return;
+            }
+            ent_append(x, k);
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const bool me = a == at;
+                A[a].s = me ? x.s : A[a].s;
+                A[a].rt = me ? x.rt : A[a].rt;
+                A[a].rp = me ? x.rp : A[a].rp;
+                A[a].pa = me ? x.pa : A[a].pa;
+                A[a].xo = me ? x.xo : A[a].xo;
+                A[a].br = me ? x.br : A[a].br;
+                aid[a] = me ? k : aid[a];
+#pragma unroll
+                for (int i = 0; i < NQ; ++i) q[a][i] = (me && i == qn) ? arr : q[a][i];  // simulation.h:74
+                nq[a] = me ? qn + 1 : nq[a];
+            }
+            av |= 1u << at;
+            am |= 1u << k;
+            return;
+        }
+        found_cold(env, k, at, was_active, arr);
+    }
+
+    // The cold path of found(): miner k is in a cold slot, or needs one (no free hot slot, or its hot
+    // slot `at` has a full queue and moves).
+    template <class Env>
+    MSIM_HD void found_cold(Env &env, uint32_t k, int at, bool was_active, int64_t arr)
+    {
+        SEL_HIT(19);
+        int c = -1;
+        ColdAct r;
+        if (at >= 0) {  // migrate hot slot `at`
+            c = free_cold();
+            if (c < 0) {
+                err |= SERR_ACT;
+                return;
+            }
+            r.x = P;
+            r.nq = 0;
+#pragma unroll
+            for (int i = 0; i < SEL_NQC; ++i) r.q[i] = T_INF;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const bool me = a == at;
+                r.x = ent_pick(me, A[a], r.x);
+                r.nq = me ? nq[a] : r.nq;
+#pragma unroll
+                for (int i = 0; i < NQ; ++i) r.q[i] = me ? q[a][i] : r.q[i];
+            }
+            r.aid = k;
+            av &= ~(1u << at);
+            take_cold(c, k);
+        } else if (was_active) {  // already cold
+#pragma unroll
+            for (int i = 0; i < NC; ++i)
+                if (cval(i) && cold_aid(i) == k) c = i;
+            r = env.cold(c);
+        } else {  // leaves the class into a cold slot
+            c = free_cold();
+            if (c < 0) {
+                err |= SERR_ACT;
+                return;
+            }
+            r.x = P;
+            r.aid = k;
+            r.nq = 0;
+#pragma unroll
+            for (int i = 0; i < SEL_NQC; ++i) r.q[i] = T_INF;
+            take_cold(c, k);
+            am |= 1u << k;
+        }
+        if (!ent_room(r.x, k)) {
+            err |= SERR_WIN;
+            return;
+        }
+        if (r.nq >= SEL_NQC) {
+            err |= SERR_QUE;
+            return;
+        }
+        ent_append(r.x, k);
+#pragma unroll
+        for (int i = 0; i < SEL_NQC; ++i) r.q[i] = i == r.nq ? arr : r.q[i];  // simulation.h:74
+        r.nq++;
+        env.cold_put(c, r);
     }
 
     // ------------------------------------------------------------------ window maintenance
@@ -175,21 +401,46 @@ struct Sel {
         }
     }
 
-    MSIM_HD void shift(int s)
+    template <class Env>
+    MSIM_HD void shift(Env &env, int s)
     {
         wb += (uint32_t)s;
         bpub -= s;
         const uint64_t fill = ~0ull << (64 - 4 * s);
+        ent_shift(P, s, fill);
 #pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            str[e] = (str[e] >> (4 * s)) | fill;
-            rt[e] -= s;
-            rp[e] -= s;
-            if (rt[e] >= WIN - s && xo[e] != SEL_NONE) {  // heights entering the window from the implicit run
-                const uint64_t mk = nib_range(WIN - s, imin(rt[e], WIN - 1));
-                str[e] = (str[e] & ~mk) | (mk & (0x1111111111111111ull * (uint64_t)xo[e]));
-            }
-            if (rt[e] < WIN) xo[e] = SEL_NONE;
+        for (int si = 0; si < NSA; ++si) ent_shift(S[si], s, fill);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ent_shift(A[a], s, fill);
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    ColdAct r = env.cold(c);
+                    ent_shift(r.x, s, fill);
+                    env.cold_put(c, r);
+                }
+        }
+    }
+
+    // Visits every valid entity (P, selfish, hot and cold actives) with f(const Ent &).
+    template <class Env, class F>
+    MSIM_HD void each(Env &env, F f) const
+    {
+        f(P);
+#pragma unroll
+        for (int si = 0; si < NS; ++si)
+            if (sval(si)) f(S[si]);
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+            if (aval(a)) f(A[a]);
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    const ColdAct r = env.cold(c);
+                    f(r.x);
+                }
         }
     }
 
@@ -198,62 +449,87 @@ struct Sel {
     template <class Env>
     MSIM_HD void fold(Env &env)
     {
-        int minrp = rt[0];
-#pragma unroll
-        for (int e = 1; e < NE; ++e)
-            if (valid(e)) minrp = imin(minrp, rp[e]);
+        SEL_HIT(14);
+        if (deep) SEL_HIT(18);
+        int minrp = P.rt;
+        each(env, [&](const Ent &x) { minrp = imin(minrp, x.rp); });
         if (minrp < 0) return;
         const int cap = imin(minrp + 1, WIN - 1);
         if (!deep) {
             int s = cap;
-#pragma unroll
-            for (int e = 1; e < NE; ++e)
-                if (valid(e)) s = imin(s, first_diff(str[e], str[0], cap - 1));
+            each(env, [&](const Ent &x) { s = imin(s, first_diff(x.s, P.s, cap - 1)); });
             if (s > 0) {
-                add_nibs(env, C_F, str[0], s);
-                shift(s);
+                SEL_HIT(17);
+                add_nibs(env, C_F, P.s, s);
+                shift(env, s);
                 return;
             }
             // The chains disagree at the lowest height: split them into two long branches.
-            const uint32_t o0 = (uint32_t)(str[0] & 15u);
-            uint32_t ob = SEL_NONE, nb = 0;
+            const uint32_t o0 = (uint32_t)(P.s & 15u);
+            uint32_t ob = SEL_NONE;
             bool three = false;
-#pragma unroll
-            for (int e = 1; e < NE; ++e)
-                if (valid(e)) {
-                    const uint32_t oe = (uint32_t)(str[e] & 15u);
-                    if (oe != o0) {
-                        nb |= 1u << e;
-                        if (ob == SEL_NONE) ob = oe;
-                        else if (oe != ob) three = true;
-                    }
+            each(env, [&](const Ent &x) {
+                const uint32_t oe = (uint32_t)(x.s & 15u);
+                if (oe != o0) {
+                    if (ob == SEL_NONE) ob = oe;
+                    else if (oe != ob) three = true;
                 }
-            if (three || nb == 0) return;
+            });
+            if (three || ob == SEL_NONE) return;
+            SEL_HIT(16);
             deep = true;
-            bm = nb;
+            set_branches(env, o0);
         }
-        uint64_t sa = 0, sb = 0;
+        uint64_t sa = P.s, sb = 0;
         bool ha = false, hb = false;
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (valid(e)) {
-                if (ebr(e)) {
-                    if (!hb) sb = str[e];
-                    hb = true;
-                } else {
-                    if (!ha) sa = str[e];
-                    ha = true;
-                }
-            }
+        each(env, [&](const Ent &x) {
+            const bool b = x.br != 0u;
+            sb = (b && !hb) ? x.s : sb;
+            sa = (!b && !ha) ? x.s : sa;
+            hb = hb || b;
+            ha = ha || !b;
+        });
+        if (!ha || !hb) return;  // cannot happen: resolve() ends deep mode when one branch is left
         int s = cap;
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (valid(e)) s = imin(s, first_diff(str[e], ebr(e) ? sb : sa, cap - 1));
+        each(env, [&](const Ent &x) { s = imin(s, first_diff(x.s, x.br ? sb : sa, cap - 1)); });
         if (s > 0) {
+            SEL_HIT(15);
             add_nibs(env, C_A, sa, s);
             add_nibs(env, C_B, sb, s);
-            shift(s);
+            shift(env, s);
         }
+    }
+
+    // Entering deep mode: branch B = every entity whose lowest window owner differs from o0.
+    template <class Env>
+    MSIM_HD void set_branches(Env &env, uint32_t o0)
+    {
+        P.br = 0;
+#pragma unroll
+        for (int si = 0; si < NSA; ++si) S[si].br = (uint32_t)(S[si].s & 15u) != o0 ? 1u : 0u;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) A[a].br = (uint32_t)(A[a].s & 15u) != o0 ? 1u : 0u;
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    ColdAct r = env.cold(c);
+                    r.x.br = (uint32_t)(r.x.s & 15u) != o0 ? 1u : 0u;
+                    env.cold_put(c, r);
+                }
+        }
+    }
+
+    // Fold when the best chain or any chain nears the top of the window (honest chains need room for the
+    // next find; an implicit run only extends with its own owner).
+    template <class Env>
+    MSIM_HD bool fold_due(Env &env, int32_t bl) const
+    {
+        int32_t r = bl;
+        each(env, [&](const Ent &x) {
+            if (x.rt < WIN) r = r > x.rt ? r : x.rt;
+        });
+        return r >= FOLD_AT;
     }
 
     // One branch left: its deep blocks are common to every chain.
@@ -262,13 +538,12 @@ struct Sel {
     {
         if (!deep) return;
         uint32_t any = 0, all = 1;
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (valid(e)) {
-                any |= ebr(e);
-                all &= ebr(e);
-            }
+        each(env, [&](const Ent &x) {
+            any |= x.br;
+            all &= x.br;
+        });
         if (any && !all) return;
+        SEL_HIT(13);
         const int src = all ? C_B : C_A;
 #pragma unroll
         for (int k = 0; k < M; ++k) {
@@ -277,105 +552,33 @@ struct Sel {
             env.set(C_B, (uint32_t)k, 0u);
         }
         deep = false;
-        bm = 0;
-    }
-
-    // ------------------------------------------------------------------ Miner::FoundBlock
-    // simulation.h:62-76 for miner k at time T. A passive miner leaves the class with its chain.
-    template <class Env>
-    MSIM_HD void found(Env &env, uint32_t k, int64_t T)
-    {
-        int et = -1;
-        if ((sm >> k) & 1u) {
+        P.br = 0;
 #pragma unroll
-            for (int si = 0; si < NS; ++si)
-                if (sidv[si] == k) et = 1 + si;
-        } else if ((am >> k) & 1u) {
+        for (int si = 0; si < NSA; ++si) S[si].br = 0;
 #pragma unroll
-            for (int a = 0; a < NA; ++a)
-                if (aid[a] == k) et = E0A + a;
-        } else {
+        for (int a = 0; a < NA; ++a) A[a].br = 0;
+        if (cm) {
 #pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                const int e = E0A + a;
-                const bool me = et < 0 && aid[a] == SEL_NONE;
-                et = me ? e : et;
-                str[e] = me ? str[0] : str[e];
-                rt[e] = me ? rt[0] : rt[e];
-                rp[e] = me ? rt[0] : rp[e];
-                pa[e] = me ? pa[0] : pa[e];
-                xo[e] = me ? xo[0] : xo[e];
-                bm = me ? ((bm & ~(1u << e)) | (ebr(0) << e)) : bm;
-                aid[a] = me ? k : aid[a];
-                nq[a] = me ? 0 : nq[a];
-                vm = me ? (vm | (1u << e)) : vm;
-            }
-            if (et >= 0) am |= 1u << k;
-        }
-        if (et < 0) {
-            err |= SERR_CAP;
-            return;
-        }
-        // Room for height rt+1: inside the window, the first implicit-run height, or the run's owner.
-        int32_t r = 0;
-        uint32_t x = SEL_NONE;
-#pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (e == et) {
-                r = rt[e];
-                x = xo[e];
-            }
-        if (r + 1 > WIN && x != k) {
-            fold(env);
-#pragma unroll
-            for (int e = 0; e < NE; ++e)
-                if (e == et) {
-                    r = rt[e];
-                    x = xo[e];
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    ColdAct r = env.cold(c);
+                    r.x.br = 0;
+                    env.cold_put(c, r);
                 }
-            if (r + 1 > WIN && x != k) {
-                err |= SERR_WIN;
-                return;
-            }
         }
-        const int64_t arr = T + env.prop(k);
-        // Append at height r + 1 of entity et (selects over the entities, see push_group).
-        const int h = r + 1;
-        const uint64_t nmask = h < WIN ? (0xFull << (4 * h)) : 0ull;
-        const uint64_t nval = h < WIN ? ((uint64_t)k << (4 * h)) : 0ull;
-#pragma unroll
-        for (int e = 1; e < NE; ++e) {
-            const bool me = e == et;
-            str[e] = me ? ((str[e] & ~nmask) | nval) : str[e];
-            xo[e] = (me && h == WIN) ? k : xo[e];
-            rt[e] = me ? h : rt[e];
-        }
-#pragma unroll
-        for (int si = 0; si < NS; ++si) {
-            if (et != 1 + si) continue;
-            const bool race = (w[si] == 1) && (bpub == r);  // simulation.h:66
-            if (race) {
-                w[si] = 0;
-                push_group(si, 2, arr);  // simulation.h:68-69: both blocks arrive at T + prop
-            } else {
-                w[si] += 1;  // simulation.h:71 (SELFISH_ARRIVAL)
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < NA; ++a)
-            if (et == E0A + a) enqueue(a, arr);  // simulation.h:74
     }
 
     // Blocks whose arrival is <= t join their chain's published prefix (UnpublishedBlocks, 79-89).
-    MSIM_HD void publish(int64_t t)
+    template <class Env>
+    MSIM_HD void publish(Env &env, int64_t t)
     {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            const int e = E0A + a;
-            if (!valid(e)) continue;
+            if (!aval(a)) continue;
             while (nq[a] > 0 && q[a][0] <= t) {
-                rp[e] += 1;
-                pa[e] = q[a][0];
+                SEL_HIT(4);
+                A[a].rp += 1;
+                A[a].pa = q[a][0];
 #pragma unroll
                 for (int i = 0; i + 1 < NQ; ++i) q[a][i] = q[a][i + 1];
                 q[a][NQ - 1] = T_INF;
@@ -384,11 +587,11 @@ struct Sel {
         }
 #pragma unroll
         for (int si = 0; si < NS; ++si) {
-            const int e = 1 + si;
-            if (!valid(e)) continue;
+            if (!sval(si)) continue;
             while (ng[si] > 0 && ga[si][0] <= t) {
-                rp[e] += gc[si][0];
-                pa[e] = ga[si][0];
+                SEL_HIT(5);
+                S[si].rp += gc[si][0];
+                S[si].pa = ga[si][0];
 #pragma unroll
                 for (int i = 0; i + 1 < NG; ++i) {
                     gc[si][i] = gc[si][i + 1];
@@ -399,87 +602,109 @@ struct Sel {
                 ng[si]--;
             }
         }
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    ColdAct r = env.cold(c);
+                    if (r.nq > 0 && r.q[0] <= t) {
+                        while (r.nq > 0 && r.q[0] <= t) {
+                            r.x.rp += 1;
+                            r.x.pa = r.q[0];
+#pragma unroll
+                            for (int i = 0; i + 1 < SEL_NQC; ++i) r.q[i] = r.q[i + 1];
+                            r.q[SEL_NQC - 1] = T_INF;
+                            r.nq--;
+                        }
+                        env.cold_put(c, r);
+                    }
+                }
+        }
     }
 
     // BestChain (main.cpp:68-82).
-    MSIM_HD SelBest best() const
+    template <class Env>
+    MSIM_HD SelBest best(Env &env) const
     {
         const uint32_t pas = hm & ~am;
-        const uint32_t pmin = pas ? (uint32_t)__builtin_ctz(pas) : 99u;
         SelBest b;
-        b.e = 0;
         b.l = -3;
         b.a = 0;
+        b.s = ~0ull;
+        b.x = SEL_NONE;
+        b.br = 0;
         uint32_t bi = 99u;
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            const bool cand = valid(e) && (e != 0 || pas != 0u);
-            const uint32_t idx = e == 0 ? pmin : owner(e);
-            const int32_t L = rp[e];
-            const int64_t A = pa[e];
-            const bool better = L > b.l || (L == b.l && (A < b.a || (A == b.a && idx < bi)));
-            if (cand && better) {
-                b.e = e;
+        auto consider = [&](const Ent &x, uint32_t idx, int32_t L) {
+            const bool better = L > b.l || (L == b.l && (x.pa < b.a || (x.pa == b.a && idx < bi)));
+            if (better) {
                 b.l = L;
-                b.a = A;
+                b.a = x.pa;
                 bi = idx;
+                b.s = x.s;
+                b.x = x.xo;
+                b.br = x.br;
             }
-        }
-        uint64_t s = 0;
-        uint32_t x = SEL_NONE, br = 0;
+        };
+        if (pas) consider(P, (uint32_t)__builtin_ctz(pas), P.rt);
 #pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (e == b.e) {
-                s = str[e];
-                x = xo[e];
-                br = ebr(e);
-            }
-        b.s = b.l >= WIN - 1 ? s : ((s & nib_upto(b.l)) | ~nib_upto(b.l));
-        b.x = b.l >= WIN ? x : SEL_NONE;
-        b.br = br;
+        for (int si = 0; si < NS; ++si)
+            if (sval(si)) consider(S[si], sidv[si], S[si].rp);
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+            if (aval(a)) consider(A[a], aid[a], A[a].rp);
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    const ColdAct r = env.cold(c);
+                    consider(r.x, r.aid, r.x.rp);
+                }
+        }
+        b.s = b.l >= WIN - 1 ? b.s : ((b.s & nib_upto(b.l)) | ~nib_upto(b.l));
+        b.x = b.l >= WIN ? b.x : SEL_NONE;
         return b;
     }
 
-    // MaybeReorg (simulation.h:124-142) of entity e to a strictly longer best chain: pop to the fork
-    // point, counting popped own blocks as stale (for P: blocks of its members), then adopt.
+    // MaybeReorg (simulation.h:124-142) of a chain to a strictly longer best chain: pop to the fork point,
+    // counting popped own blocks as stale (for the class: blocks of its members, `pas`), then adopt.
     template <class Env>
-    MSIM_HD void reorg(Env &env, int e, const SelBest &B, uint32_t pas)
+    MSIM_HD void reorg_ent(Env &env, Ent &x, bool is_p, uint32_t own, const SelBest &B, uint32_t pas)
     {
-        const bool same = !deep || ebr(e) == B.br;
-        const int top = imin(rt[e], WIN - 1);
-        const int d = same ? first_diff(str[e], B.s, top) : 0;
-        const int32_t beyond = rt[e] >= WIN ? rt[e] - (WIN - 1) : 0;
-        const bool popb = beyond > 0 && (!same || d <= top || xo[e] != B.x);
-        if (e == 0) {
+        const bool same = !deep || x.br == B.br;
+        const int top = imin(x.rt, WIN - 1);
+        const int d = same ? first_diff(x.s, B.s, top) : 0;
+        const int32_t beyond = x.rt >= WIN ? x.rt - (WIN - 1) : 0;
+        const bool popb = beyond > 0 && (!same || d <= top || x.xo != B.x);
+        if (!same) SEL_HIT(11);
+        if (is_p) {
+            SEL_HIT(7);
+            if (d <= top) SEL_HIT(8);
             for (int j = d; j <= top; ++j) {
-                const uint32_t o = (uint32_t)(str[0] >> (4 * j)) & 15u;
+                const uint32_t o = (uint32_t)(x.s >> (4 * j)) & 15u;
                 if ((pas >> o) & 1u) env.add(C_S, o, 1u);
             }
-            if (popb && ((pas >> xo[0]) & 1u)) env.add(C_S, xo[0], (uint32_t)beyond);
+            if (popb && ((pas >> x.xo) & 1u)) env.add(C_S, x.xo, (uint32_t)beyond);
             if (!same) {
 #pragma unroll
                 for (int k = 0; k < M; ++k)
-                    if ((pas >> k) & 1u) env.add(C_S, (uint32_t)k, env.get(ebr(0) ? C_B : C_A, (uint32_t)k));
+                    if ((pas >> k) & 1u) env.add(C_S, (uint32_t)k, env.get(x.br ? C_B : C_A, (uint32_t)k));
             }
         } else {
-            const uint32_t o = owner(e);
-            uint32_t c = (uint32_t)count_nib(str[e], o, nib_range(d, top));
-            if (popb && xo[e] == o) c += (uint32_t)beyond;
-            if (!same) c += env.get(ebr(e) ? C_B : C_A, o);
-            if (c) env.add(C_S, o, c);
+            SEL_HIT(9);
+            uint32_t c = (uint32_t)count_nib(x.s, own, nib_range(d, top));
+            if (popb && x.xo == own) c += (uint32_t)beyond;
+            if (!same) c += env.get(x.br ? C_B : C_A, own);
+            if (c) {
+                SEL_HIT(10);
+                env.add(C_S, own, c);
+            }
         }
-        str[e] = B.s;
-        rt[e] = B.l;
-        rp[e] = B.l;
-        pa[e] = B.a;
-        xo[e] = B.x;
-        bm = (bm & ~(1u << e)) | (B.br << e);
-        if (e >= 1 && e < E0A) {
-            w[e - 1] = 0;
-            ng[e - 1] = 0;
-        } else if (e >= E0A) {
-            nq[e - E0A] = 0;
-        }
+        x.s = B.s;
+        x.rt = B.l;
+        x.rp = B.l;
+        x.pa = B.a;
+        x.xo = B.x;
+        x.br = B.br;
     }
 
     // NotifyBestChain for every miner (main.cpp:165-167 -> simulation.h:177-180): Reveal, then Reorg.
@@ -488,10 +713,10 @@ struct Sel {
     {
 #pragma unroll
         for (int si = 0; si < NS; ++si) {
-            const int e = 1 + si;
-            if (valid(e) && B.l <= rt[e]) {  // MaybeSelfishReveal (simulation.h:149-174)
-                const int32_t sc = w[si], lead = rt[e] - B.l;
+            if (sval(si) && B.l <= S[si].rt) {  // MaybeSelfishReveal (simulation.h:149-174)
+                const int32_t sc = w[si], lead = S[si].rt - B.l;
                 if (sc > lead) {
+                    SEL_HIT(6);
                     int32_t rc = sc - lead;
                     if (sc > 1 && lead == 1) rc = sc;
                     push_group(si, rc, t + env.prop(sidv[si]));
@@ -500,75 +725,132 @@ struct Sel {
             }
         }
         const uint32_t pas = hm & ~am;
+        if (B.l > P.rt) reorg_ent(env, P, true, 0u, B, pas);
 #pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (valid(e) && B.l > rt[e]) reorg(env, e, B, pas);
-    }
-
-    // An active miner whose chain is the class's chain again, all published, rejoins the class.
-    MSIM_HD void merge()
-    {
+        for (int si = 0; si < NS; ++si)
+            if (sval(si) && B.l > S[si].rt) {
+                reorg_ent(env, S[si], false, sidv[si], B, pas);
+                w[si] = 0;
+                ng[si] = 0;
+            }
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-            const int e = E0A + a;
-            if (valid(e) && rp[e] == rt[e] && rt[e] == rt[0] && str[e] == str[0] && xo[e] == xo[0] &&
-                ebr(e) == ebr(0)) {
-                vm &= ~(1u << e);
-                am &= ~(1u << aid[a]);
-                aid[a] = SEL_NONE;
+        for (int a = 0; a < NA; ++a)
+            if (aval(a) && B.l > A[a].rt) {
+                reorg_ent(env, A[a], false, aid[a], B, pas);
                 nq[a] = 0;
             }
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    ColdAct r = env.cold(c);
+                    if (B.l > r.x.rt) {
+                        reorg_ent(env, r.x, false, r.aid, B, pas);
+                        r.nq = 0;
+                        env.cold_put(c, r);
+                    }
+                }
+        }
+    }
+
+    // Active miners whose chain is the class's chain again rejoin the class.
+    template <class Env>
+    MSIM_HD void merge(Env &env)
+    {
+#pragma unroll
+        for (int a = 0; a < NA; ++a)
+            if (aval(a) && ent_same_as_p(A[a], P)) {
+                SEL_HIT(12);
+                av &= ~(1u << a);
+                am &= ~(1u << aid[a]);
+                nq[a] = 0;
+            }
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    const ColdAct r = env.cold(c);
+                    if (ent_same_as_p(r.x, P)) {
+                        cm &= ~(1u << c);
+                        am &= ~(1u << r.aid);
+                    }
+                }
         }
     }
 
     // EarliestArrival (main.cpp:99-112) over NextArrival (simulation.h:92-102); withheld blocks
     // (SELFISH_ARRIVAL) never bring the next event forward.
-    MSIM_HD int64_t earliest(int64_t t) const
+    template <class Env>
+    MSIM_HD int64_t earliest(Env &env, int64_t t) const
     {
         int64_t ea = T_INF;
 #pragma unroll
         for (int a = 0; a < NA; ++a)
-            if (valid(E0A + a) && nq[a] > 0) ea = lmin(ea, q[a][0]);
+            if (aval(a) && nq[a] > 0) ea = lmin(ea, q[a][0]);
 #pragma unroll
         for (int si = 0; si < NS; ++si)
-            if (valid(1 + si) && ng[si] > 0 && ga[si][0] > t) ea = lmin(ea, ga[si][0]);
+            if (sval(si) && ng[si] > 0 && ga[si][0] > t) ea = lmin(ea, ga[si][0]);
+        if (cm) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                if (cval(c)) {
+                    const ColdAct r = env.cold(c);
+                    if (r.nq > 0) ea = lmin(ea, r.q[0]);
+                }
+        }
         return ea;
     }
 
-    // RunSimulation (main.cpp:128-192) for one run.
-    template <class Env, class Src>
-    MSIM_HD void run(Env &env, Src &src, int64_t D, SelOut &out)
+    // RunSimulation (main.cpp:128-192) for one run, as begin / step (one event) / finish so that a
+    // kernel can interleave its own work between events.
+    int64_t t_, nbt_;
+    uint32_t kn_;
+    template <class Src>
+    MSIM_HD void begin(Src &src)
     {
-        uint32_t I = 0, kn = 0;
-        if (!src.next(I, kn)) err |= SERR_DRAWS;
-        int64_t nbt = (int64_t)I;  // main.cpp:138
-        int64_t t = 0;
-        while (t < D && err == 0) {  // main.cpp:150
-            while (t == nbt) {       // main.cpp:153-157
-                if (kn >= (uint32_t)M) {
-                    err |= SERR_PICK;
-                    break;
-                }
-                found(env, kn, t);
-                if (!src.next(I, kn)) {
-                    err |= SERR_DRAWS;
-                    break;
-                }
-                nbt += (int64_t)I;
+        uint32_t I = 0;
+        kn_ = 0;
+        if (!src.next(I, kn_)) err |= SERR_DRAWS;
+        nbt_ = (int64_t)I;  // main.cpp:138
+        t_ = 0;
+    }
+    // One iteration of main.cpp:150-182 at cur_time = t_. Returns false once the loop has ended.
+    template <class Env, class Src>
+    MSIM_HD bool step(Env &env, Src &src, int64_t D)
+    {
+        if (!(t_ < D && err == 0)) return false;  // main.cpp:150
+        const int64_t t = t_;
+        while (t == nbt_) {  // main.cpp:153-157
+            SEL_HIT(0);
+            if (kn_ >= (uint32_t)M) {
+                err |= SERR_PICK;
+                break;
             }
-            if (err) break;
-            publish(t);
-            const SelBest B = best();  // main.cpp:164
-            notify(env, t, B);         // main.cpp:165-167
-            merge();
-            bpub = B.l;                // main.cpp:171
-            resolve(env);
-            if (B.l >= FOLD_AT) fold(env);
-            t = lmin(nbt, earliest(t));  // main.cpp:176-182
+            found(env, kn_, t);
+            uint32_t I = 0;
+            if (!src.next(I, kn_)) {
+                err |= SERR_DRAWS;
+                break;
+            }
+            nbt_ += (int64_t)I;
         }
-        // main.cpp:185-189: BestChain at the end of the run, no notify.
-        publish(D);
-        const SelBest B = best();
+        if (err) return false;
+        publish(env, t);
+        const SelBest B = best(env);  // main.cpp:164
+        notify(env, t, B);            // main.cpp:165-167
+        merge(env);
+        bpub = B.l;                   // main.cpp:171
+        resolve(env);
+        if (fold_due(env, B.l)) fold(env);
+        t_ = lmin(nbt_, earliest(env, t));  // main.cpp:176-182
+        return true;
+    }
+    // main.cpp:185-189: BestChain at the end of the run, no notify.
+    template <class Env>
+    MSIM_HD void finish(Env &env, int64_t D, SelOut &out)
+    {
+        publish(env, D);
+        const SelBest B = best(env);
         const int top = imin(B.l, WIN - 1);
 #pragma unroll
         for (int k = 0; k < M; ++k) {
@@ -580,6 +862,14 @@ struct Sel {
         }
         out.best_height = wb + (uint32_t)B.l;
         out.err = err;
+    }
+    template <class Env, class Src>
+    MSIM_HD void run(Env &env, Src &src, int64_t D, SelOut &out)
+    {
+        begin(src);
+        while (step(env, src, D)) {
+        }
+        finish(env, D, out);
     }
 };
 

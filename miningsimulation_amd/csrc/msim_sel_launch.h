@@ -23,13 +23,14 @@
 
 namespace msim {
 
-constexpr uint32_t SEL_LUT = 128;
 constexpr uint32_t SEL_TILE = 32;  // words per (run, tile)
 
-// Capacity classes of E1 (active honest miners, reveal groups, in-flight blocks per active miner).
-// Measured on the host engine over the configs[3] grid: SMALL flags ~1/60 runs at 1 s
-// propagation and almost every run at >= 10 s; LARGE flags none at 30 s.
+// Capacity classes of E1 (hot active slots, reveal groups, in-flight blocks per hot active slot), all
+// backed by SEL_NC cold slots in global memory (msim_sel.h): SMALL = (2, 4, 2), LARGE = (3, 8, 3). A run
+// that exceeds them anyway is recomputed by E2, which costs a whole run-year on one lane, so E1 must
+// practically never flag.
 enum : uint32_t { SEL_SMALL = 0, SEL_LARGE = 1 };
+constexpr int SEL_NC = 4;
 constexpr int64_t SEL_SMALL_MAX_PROP = 2000;  // ms: networks up to this propagation use SEL_SMALL
 
 // One network of a launch (a sweep point).
@@ -42,8 +43,12 @@ struct SelParams {
     uint32_t m;
     uint32_t ns;         // selfish miners
     uint32_t sids[SEL_MAXS];
-    uint32_t pad;
-    uint8_t lut[SEL_LUT];  // word code -> finder (15: PickFinder falls through, simulation.h:220)
+    uint32_t uniform_prop;  // 1: every miner has prop[0]
+    // word code -> finder = #{k : ccum[k] <= code}: W = 100 words carry q = floor(u / PERC_MULTIPLIER)
+    // and ccum = cumulative percentages (first k with cum_k > q, simulation.h:217-218); weighted words
+    // carry the finder and ccum[k] = k + 1. Unused entries 0xFFFFFFFF; a result >= m falls through.
+    uint32_t ccum[MAXM];
+    uint32_t pad2;
 };
 
 struct WordArgs {
@@ -78,6 +83,8 @@ struct SelArgs {
     uint32_t *err_list;     // err_cap codes point * rpp + run
     uint32_t err_cap;
     uint32_t force_retry;   // test switch (MSIM_SEL_FORCE_RETRY): E1 flags every run, E2 computes all
+    ColdAct *cold;          // cold slots: [SEL_NC][cold_lanes] (E1 lane = point-list slot * sn + run; E2 lane)
+    size_t cold_lanes;
 };
 
 struct SelLayout {

@@ -19,11 +19,17 @@
  *   main.cpp:128-192        RunSimulation
  *
  * Pinning: the reference cannot be built here unmodified (libstdc++ 11 lacks the C++20 chrono
- * operator<< used at simulation.h:228 / main.cpp:225), so this restatement is pinned against
+ * operator<< used at simulation.h:228 / main.cpp:225), so this restatement is pinned against what the
+ * reference itself holds or produced (tests/test_oracle.py, tests/test_gpu_selfish.py):
  *   (1) the reference's own known-answer test, test.cpp:213-367 TestSelfishStrategy (tests/golden),
- *   (2) reference outputs recorded in this container by the survey (RNG, interval,
- *       picker KATs and two 64-run FNV hashes of per-run MinerStats),
- *   (3) the README's published 32768-run averages (statistical).
+ *   (2) reference outputs recorded in this container by the survey: RNG,
+ *       NextBlockInterval and PickFinder streams, and the per-miner found/stale counters of run 0 of two
+ *       honest networks (10 s and 1 s propagation, a full year). The two 64-run FNV-1a hashes Appendix B
+ *       also lists do NOT reproduce under its stated convention (this oracle gives 61f4602de20bc73c and
+ *       7da94b60a84b8bcb; DESIGN.md §5 lists the conventions tried) and are not used as a pin;
+ *   (3) the README's published 32768-run averages (statistical), including the only published selfish
+ *       result (README.md:98-99), which pins whole selfish runs of the reference;
+ *   (4) glibc's own log1p / llround (tests/native/draws_check.cpp, bit for bit).
  *
  * Arithmetic: glibc log1p / llround exactly as the reference calls them (compile with
  * -ffp-contract=off; x86-64 baseline has no FMA, like the reference build line README.md:32).

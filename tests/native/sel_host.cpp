@@ -14,10 +14,13 @@ namespace {
 struct HostEnv {
     const int64_t *props;
     uint32_t c[4][MAXM];
+    ColdAct cs[8];
     int64_t prop(uint32_t k) const { return props[k]; }
     uint32_t get(int a, uint32_t k) const { return c[a][k]; }
     void add(int a, uint32_t k, uint32_t v) { c[a][k] += v; }
     void set(int a, uint32_t k, uint32_t v) { c[a][k] = v; }
+    ColdAct cold(int i) const { return cs[i]; }
+    void cold_put(int i, const ColdAct &r) { cs[i] = r; }
 };
 
 // Draws exactly as the reference's loop makes them (simulation.h:205-221), through the same packed
@@ -40,13 +43,14 @@ struct HostSrc {
     }
 };
 
-template <int M, int NS, int NA, int NG, int NQ>
+template <int M, int NS, int NA, int NG, int NQ, int NC>
 void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
 {
     HostEnv env;
     env.props = prop;
     memset(env.c, 0, sizeof(env.c));
-    Sel<M, NS, NA, NG, NQ> s;
+    memset(env.cs, 0, sizeof(env.cs));
+    Sel<M, NS, NA, NG, NQ, NC> s;
     s.init((uint32_t)M, sids);
     s.run(env, src, D, o);
 }
@@ -54,23 +58,18 @@ void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D,
 template <int M, int NS>
 void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
 {
-    if (caps == 0) run_one<M, NS, 2, 4, 2>(prop, sids, src, D, o);
-    else if (caps == 1) run_one<M, NS, 8, 16, 8>(prop, sids, src, D, o);
-    else if (caps == 2) run_one<M, NS, 1, 1, 1>(prop, sids, src, D, o);  // tiny: exercises the error paths
-#ifdef SEL_CAP_PROBE
-    else if (caps == 3) run_one<M, NS, 4, 4, 2>(prop, sids, src, D, o);
-    else if (caps == 4) run_one<M, NS, 2, 8, 2>(prop, sids, src, D, o);
-    else if (caps == 5) run_one<M, NS, 2, 4, 4>(prop, sids, src, D, o);
-    else if (caps == 6) run_one<M, NS, 3, 6, 3>(prop, sids, src, D, o);
-    else if (caps == 7) run_one<M, NS, 4, 8, 3>(prop, sids, src, D, o);
-    else if (caps == 8) run_one<M, NS, 3, 4, 2>(prop, sids, src, D, o);
-    else if (caps == 9) run_one<M, NS, 3, 6, 2>(prop, sids, src, D, o);
-#endif
+    // 0 / 3: the device's SMALL / LARGE classes (msim_sel_launch.h), 1: retry capacities,
+    // 2: one hot slot of everything (the cold paths run constantly), 4: no cold slots (error paths)
+    if (caps == 0) run_one<M, NS, 2, 4, 2, 4>(prop, sids, src, D, o);
+    else if (caps == 1) run_one<M, NS, 4, 16, 4, 6>(prop, sids, src, D, o);
+    else if (caps == 2) run_one<M, NS, 1, 4, 1, 6>(prop, sids, src, D, o);
+    else if (caps == 3) run_one<M, NS, 3, 8, 3, 4>(prop, sids, src, D, o);
+    else run_one<M, NS, 1, 1, 1, 0>(prop, sids, src, D, o);
 }
 
 }  // namespace
 
-// weights[m] summing to W, prop[m], selfish[m]; caps 0 = fast kernel capacities, 1 = retry, 2 = tiny.
+// weights[m] summing to W, prop[m], selfish[m]; caps: see run_caps.
 extern "C" int sel_run(const uint64_t *weights, const int64_t *prop, const uint8_t *selfish, int m, uint64_t W,
                        int64_t duration_ms, uint32_t seed_i, uint32_t seed_p, int caps, uint32_t *found,
                        uint32_t *stale, uint32_t *best_height, uint32_t *err)
