@@ -42,6 +42,36 @@ def w_blk(m: int) -> int:
     return 140 + 4 * math.ceil(math.log2(max(m, 2)))
 
 
+# SURVEY §8(d) calibration of the oracle port against the reference binary: both at 8 threads in the
+# same 8-vCPU build container (Intel Xeon @ 2.1 GHz), c2 at 32 768 runs: the unmodified reference
+# measured 609 run-years/s; the port measured 352.1 run-years/s (oracle_cli time c2
+# 32768 8, 93.08 s). A port figure divided by this ratio estimates the reference binary on the same cores.
+PORT_TO_REFERENCE = round(352.056 / 609.0, 4)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def host_threads() -> tuple[int, str]:
+    """Every CPU this process may run on, bounded by the CPU share the host allots to one GPU job (the GPU
+    box exports OMP_NUM_THREADS = its per-GPU share; nproc there shows the whole machine)."""
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and 0 < int(share) < cpus:
+        return int(share), f"{share} of {cpus} visible CPUs (the host's per-GPU CPU share, OMP_NUM_THREADS)"
+    return cpus, f"all {cpus} visible CPUs"
+
+
 def cpu_baseline(preset: str, sample_runs: int, threads: int, target_s: float = 15.0) -> dict:
     from oracle import pyoracle
 
@@ -64,6 +94,11 @@ def cpu_baseline(preset: str, sample_runs: int, threads: int, target_s: float = 
         "kind": "port",
         "sample": f"{sample_runs} runs x 365.2425 d of preset {preset} (oracle/msim_oracle.c, explicit chains as "
                   f"in the reference, {threads} pthreads), {rec['seconds']:.1f} s wall",
+        "cpu_model": cpu_model(),
+        "port_to_reference_ratio": PORT_TO_REFERENCE,
+        "reference_equivalent": round(rec["run_years_per_s"] / PORT_TO_REFERENCE, 2),
+        "calibration": "port 352.1 vs reference binary 609 run-years/s, c2, 32768 runs, 8 threads, same container "
+                       "(BASELINE.md §2); reference_equivalent = value / ratio",
     }
 
 
@@ -197,8 +232,9 @@ def main() -> None:
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = max(1, min(16, os.cpu_count() or 1))
+            threads, how = host_threads()
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_runs, threads)
+            line["cpu_baseline"]["cores_note"] = how
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

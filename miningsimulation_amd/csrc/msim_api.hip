@@ -46,10 +46,9 @@ struct msim_config {
     std::vector<uint64_t> wperc;
     std::vector<int64_t> wprop;
     std::vector<std::pair<int, void *>> wtables;  // per device: pick, fast-threshold, prop, log, jump tables
-    // Networks with selfish miners (msim_sel.h entity engine): parameter block, capacity class.
+    // Networks with selfish miners (msim_sel.h entity engine): parameter block.
     bool sel = false;
     msim::SelParams sp;
-    uint32_t sel_caps = msim::SEL_SMALL;
     std::vector<std::pair<int, void *>> stables;  // per device: SelParams + point list {0}
 };
 
@@ -61,12 +60,12 @@ struct msim_sweep {
     std::mutex mu;
     std::vector<std::pair<int, void *>> dev;  // (device, SimParams[n_points])
     // Entity-engine sweeps (some point has a selfish miner): every point's SelParams, the points grouped
-    // by (capacity class, selfish class), one draw pass per slice shared by all points.
+    // by selfish class, one draw pass per slice shared by all points.
     bool sel = false;
     int64_t max_duration = 0;
     std::vector<msim::SelParams> sps;
     struct Group {
-        uint32_t caps, nscls;
+        uint32_t nscls;
         std::vector<uint32_t> points;
     };
     std::vector<Group> groups;
@@ -361,7 +360,7 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
 }
 
 struct SelGroupDev {
-    uint32_t caps, nscls, nlist;
+    uint32_t nscls, nlist;
     const uint32_t *plist;
 };
 
@@ -425,7 +424,7 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
             if (!g.nlist) continue;
             a.plist = g.plist;
             a.nlist = g.nlist;
-            if (launch_sel(a, m, g.nscls, g.caps, s) != hipSuccess) return MSIM_E_HIP;
+            if (launch_sel(a, m, g.nscls, s) != hipSuccess) return MSIM_E_HIP;
         }
         event(engine_events);
     }
@@ -533,10 +532,6 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         if (sel) {
             c->sel = true;
             build_sel_params(miners, n, duration_ms, total_weight, &c->sp);
-            int64_t maxp = 0;
-            for (uint32_t k = 0; k < n; ++k) maxp = miners[k].propagation_ms > maxp ? miners[k].propagation_ms : maxp;
-            c->sel_caps = maxp <= msim::SEL_SMALL_MAX_PROP ? msim::SEL_SMALL : msim::SEL_LARGE;
-            if (getenv("MSIM_SEL_LARGE")) c->sel_caps = msim::SEL_LARGE;
             c->p.duration_ms = duration_ms;
             c->p.m = (int32_t)n;
             c->p.selfish = (int32_t)c->sp.sids[0];
@@ -680,7 +675,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         msim::WordArgs da;
         rc = sel_word_args(c, cfg->sp, w, &da);
         if (rc) return rc;
-        std::vector<SelGroupDev> groups{{cfg->sel_caps, msim::sel_ns_class(cfg->sp.ns), 1u, plist}};
+        std::vector<SelGroupDev> groups{{msim::sel_ns_class(cfg->sp.ns), 1u, plist}};
         Timing &tm = timing();
         std::unique_lock<std::mutex> lk(tm.mu);
         hipEvent_t lb = nullptr, le = nullptr;
@@ -886,33 +881,27 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
         w->sel = w->sel || cfgs[i]->sel;
     }
     if (w->sel) {
-        // every point on the entity engine; points grouped by (capacity class, selfish class)
+        // every point on the entity engine; points grouped by selfish class
         for (uint32_t i = 0; i < n_points; ++i) {
             const msim_config *c = cfgs[i];
             msim::SelParams sp;
-            uint32_t caps = c->sel_caps;
             if (c->sel) {
                 sp = c->sp;
             } else {
                 std::vector<msim_miner> ms(c->n);
-                int64_t maxp = 0;
-                for (uint32_t k = 0; k < c->n; ++k) {
-                    ms[k] = msim_miner{c->ids[k], c->perc[k], c->prop[k], 0};
-                    maxp = c->prop[k] > maxp ? c->prop[k] : maxp;
-                }
+                for (uint32_t k = 0; k < c->n; ++k) ms[k] = msim_miner{c->ids[k], c->perc[k], c->prop[k], 0};
                 build_sel_params(ms.data(), c->n, c->p.duration_ms, 100, &sp);
-                caps = maxp <= msim::SEL_SMALL_MAX_PROP ? msim::SEL_SMALL : msim::SEL_LARGE;
             }
             w->sps.push_back(sp);
             w->max_duration = sp.duration_ms > w->max_duration ? sp.duration_ms : w->max_duration;
             const uint32_t nc = msim::sel_ns_class(sp.ns);
             bool placed = false;
             for (auto &g : w->groups)
-                if (g.caps == caps && g.nscls == nc) {
+                if (g.nscls == nc) {
                     g.points.push_back(i);
                     placed = true;
                 }
-            if (!placed) w->groups.push_back({caps, nc, {i}});
+            if (!placed) w->groups.push_back({nc, {i}});
         }
         w->tab_cfg = cfgs[0];
     }
@@ -971,7 +960,7 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
         std::vector<SelGroupDev> groups;
         const uint32_t *pl = (const uint32_t *)((const char *)d + pb);
         for (const auto &gr : sm->groups) {
-            groups.push_back({gr.caps, gr.nscls, (uint32_t)gr.points.size(), pl});
+            groups.push_back({gr.nscls, (uint32_t)gr.points.size(), pl});
             pl += gr.points.size();
         }
         msim::WordArgs da;

@@ -106,12 +106,12 @@ hipError_t launch_sweep(const SweepArgs &a)
     }
 }
 
-hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, uint32_t caps, hipStream_t s)
+hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s)
 {
     switch (m) {
 #define CASE(MM) \
     case MM:     \
-        return launch_sel_m##MM(a, ns_class, caps, s);
+        return launch_sel_m##MM(a, ns_class, s);
         MSIM_FOR_EACH_M(CASE)
 #undef CASE
     default:

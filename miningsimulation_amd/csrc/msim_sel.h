@@ -103,7 +103,7 @@ MSIM_HD void ent_reset(Ent &x)
 
 // Room for a block of owner o at height rt + 1: inside the window, the first implicit-run height, or an
 // implicit run of the same owner.
-MSIM_HD bool ent_room(const Ent &x, uint32_t o) { return x.rt + 1 <= WIN || x.xo == o; }
+MSIM_HD bool ent_room(const Ent &x, uint32_t o) { return (x.rt + 1 <= WIN) | (x.xo == o); }
 
 MSIM_HD void ent_append(Ent &x, uint32_t o)
 {
@@ -142,11 +142,13 @@ MSIM_HD Ent ent_pick(bool c, const Ent &a, const Ent &b)
 // An active miner whose chain is the class's chain again, all published, rejoins the class.
 MSIM_HD bool ent_same_as_p(const Ent &x, const Ent &P)
 {
-    return x.rp == x.rt && x.rt == P.rt && x.s == P.s && x.xo == P.xo && x.br == P.br;
+    // bitwise, not short-circuit: these run for most lanes of every wave iteration (no branches)
+    return (x.rp == x.rt) & (x.rt == P.rt) & (x.s == P.s) & (x.xo == P.xo) & (x.br == P.br);
 }
 
 // Env: int64_t prop(uint32_t k); uint32_t get(int arr, uint32_t k); void add(int arr, uint32_t k, uint32_t v);
-//      void set(int arr, uint32_t k, uint32_t v); ColdAct cold(int c); void cold_put(int c, const ColdAct &).
+//      void set(int arr, uint32_t k, uint32_t v); ColdAct cold(int c); void cold_put(int c, const ColdAct &);
+//      bool fold_vote(bool due)  (fold now: at least `due`; may be true when not due).
 // Src: bool next(uint32_t &interval_ms, uint32_t &finder)  (finder >= M: PickFinder fell through).
 template <int M, int NS, int NA, int NG, int NQ, int NC>
 struct Sel {
@@ -266,7 +268,7 @@ struct Sel {
                     err |= SERR_WIN;
                     return;
                 }
-                const bool race = (w[si] == 1) && (bpub == S[si].rt);  // simulation.h:66
+                const bool race = (w[si] == 1) & (bpub == S[si].rt);  // simulation.h:66
                 if (race) {
                     w[si] = 0;
                     push_group(si, 2, arr);  // simulation.h:68-69: both blocks arrive at T + prop
@@ -423,57 +425,57 @@ struct Sel {
         }
     }
 
-    // Visits every valid entity (P, selfish, hot and cold actives) with f(const Ent &).
+    // Visits every entity slot with f(const Ent &, bool valid): the register-resident slots without a
+    // branch (f selects on `valid`), the cold slots only when the lane has any.
     template <class Env, class F>
     MSIM_HD void each(Env &env, F f) const
     {
-        f(P);
+        f(P, true);
 #pragma unroll
-        for (int si = 0; si < NS; ++si)
-            if (sval(si)) f(S[si]);
+        for (int si = 0; si < NS; ++si) f(S[si], sval(si));
 #pragma unroll
-        for (int a = 0; a < NA; ++a)
-            if (aval(a)) f(A[a]);
+        for (int a = 0; a < NA; ++a) f(A[a], aval(a));
         if (cm) {
 #pragma unroll
             for (int c = 0; c < NC; ++c)
                 if (cval(c)) {
                     const ColdAct r = env.cold(c);
-                    f(r.x);
+                    f(r.x, true);
                 }
         }
     }
 
     // Fold the lowest window heights that every chain holds (all published) into the settled counters,
     // or, during a two-branch episode, into the deep-branch counters of each branch.
+    // An early fold (not `due`) only shifts: splitting into deep mode waits until the lane needs room.
     template <class Env>
-    MSIM_HD void fold(Env &env)
+    MSIM_HD void fold(Env &env, bool due)
     {
         SEL_HIT(14);
         if (deep) SEL_HIT(18);
         int minrp = P.rt;
-        each(env, [&](const Ent &x) { minrp = imin(minrp, x.rp); });
+        each(env, [&](const Ent &x, bool v) { minrp = v ? imin(minrp, x.rp) : minrp; });
         if (minrp < 0) return;
         const int cap = imin(minrp + 1, WIN - 1);
         if (!deep) {
             int s = cap;
-            each(env, [&](const Ent &x) { s = imin(s, first_diff(x.s, P.s, cap - 1)); });
+            each(env, [&](const Ent &x, bool v) { s = v ? imin(s, first_diff(x.s, P.s, cap - 1)) : s; });
             if (s > 0) {
                 SEL_HIT(17);
                 add_nibs(env, C_F, P.s, s);
                 shift(env, s);
                 return;
             }
+            if (!due) return;
             // The chains disagree at the lowest height: split them into two long branches.
             const uint32_t o0 = (uint32_t)(P.s & 15u);
             uint32_t ob = SEL_NONE;
             bool three = false;
-            each(env, [&](const Ent &x) {
+            each(env, [&](const Ent &x, bool v) {
                 const uint32_t oe = (uint32_t)(x.s & 15u);
-                if (oe != o0) {
-                    if (ob == SEL_NONE) ob = oe;
-                    else if (oe != ob) three = true;
-                }
+                const bool d = v & (oe != o0);
+                three = three | (d & (ob != SEL_NONE) & (oe != ob));
+                ob = (d & (ob == SEL_NONE)) ? oe : ob;
             });
             if (three || ob == SEL_NONE) return;
             SEL_HIT(16);
@@ -482,16 +484,16 @@ struct Sel {
         }
         uint64_t sa = P.s, sb = 0;
         bool ha = false, hb = false;
-        each(env, [&](const Ent &x) {
+        each(env, [&](const Ent &x, bool v) {
             const bool b = x.br != 0u;
-            sb = (b && !hb) ? x.s : sb;
-            sa = (!b && !ha) ? x.s : sa;
-            hb = hb || b;
-            ha = ha || !b;
+            sb = (v & b & !hb) ? x.s : sb;
+            sa = (v & !b & !ha) ? x.s : sa;
+            hb = hb | (v & b);
+            ha = ha | (v & !b);
         });
         if (!ha || !hb) return;  // cannot happen: resolve() ends deep mode when one branch is left
         int s = cap;
-        each(env, [&](const Ent &x) { s = imin(s, first_diff(x.s, x.br ? sb : sa, cap - 1)); });
+        each(env, [&](const Ent &x, bool v) { s = v ? imin(s, first_diff(x.s, x.br ? sb : sa, cap - 1)) : s; });
         if (s > 0) {
             SEL_HIT(15);
             add_nibs(env, C_A, sa, s);
@@ -526,9 +528,7 @@ struct Sel {
     MSIM_HD bool fold_due(Env &env, int32_t bl) const
     {
         int32_t r = bl;
-        each(env, [&](const Ent &x) {
-            if (x.rt < WIN) r = r > x.rt ? r : x.rt;
-        });
+        each(env, [&](const Ent &x, bool v) { r = (v & (x.rt < WIN) & (x.rt > r)) ? x.rt : r; });
         return r >= FOLD_AT;
     }
 
@@ -538,9 +538,9 @@ struct Sel {
     {
         if (!deep) return;
         uint32_t any = 0, all = 1;
-        each(env, [&](const Ent &x) {
-            any |= x.br;
-            all &= x.br;
+        each(env, [&](const Ent &x, bool v) {
+            any |= v ? x.br : 0u;
+            all &= v ? x.br : 1u;
         });
         if (any && !all) return;
         SEL_HIT(13);
@@ -572,34 +572,39 @@ struct Sel {
     template <class Env>
     MSIM_HD void publish(Env &env, int64_t t)
     {
+        // One pop per queue is branch-free (most lanes of a wave need it); further pops are rare.
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            if (!aval(a)) continue;
-            while (nq[a] > 0 && q[a][0] <= t) {
-                SEL_HIT(4);
-                A[a].rp += 1;
-                A[a].pa = q[a][0];
+            for (int rep = 0;; ++rep) {
+                const bool p = aval(a) & (nq[a] > 0) & (q[a][0] <= t);
+                if (rep > 0 && !p) break;
+                if (p) SEL_HIT(4);
+                A[a].rp += p ? 1 : 0;
+                A[a].pa = p ? q[a][0] : A[a].pa;
 #pragma unroll
-                for (int i = 0; i + 1 < NQ; ++i) q[a][i] = q[a][i + 1];
-                q[a][NQ - 1] = T_INF;
-                nq[a]--;
+                for (int i = 0; i + 1 < NQ; ++i) q[a][i] = p ? q[a][i + 1] : q[a][i];
+                q[a][NQ - 1] = p ? T_INF : q[a][NQ - 1];
+                nq[a] -= p ? 1 : 0;
+                if (!(aval(a) & (nq[a] > 0) & (q[a][0] <= t))) break;
             }
         }
 #pragma unroll
         for (int si = 0; si < NS; ++si) {
-            if (!sval(si)) continue;
-            while (ng[si] > 0 && ga[si][0] <= t) {
-                SEL_HIT(5);
-                S[si].rp += gc[si][0];
-                S[si].pa = ga[si][0];
+            for (int rep = 0;; ++rep) {
+                const bool p = sval(si) & (ng[si] > 0) & (ga[si][0] <= t);
+                if (rep > 0 && !p) break;
+                if (p) SEL_HIT(5);
+                S[si].rp += p ? gc[si][0] : 0;
+                S[si].pa = p ? ga[si][0] : S[si].pa;
 #pragma unroll
                 for (int i = 0; i + 1 < NG; ++i) {
-                    gc[si][i] = gc[si][i + 1];
-                    ga[si][i] = ga[si][i + 1];
+                    gc[si][i] = p ? gc[si][i + 1] : gc[si][i];
+                    ga[si][i] = p ? ga[si][i + 1] : ga[si][i];
                 }
-                gc[si][NG - 1] = 0;
-                ga[si][NG - 1] = T_INF;
-                ng[si]--;
+                gc[si][NG - 1] = p ? 0 : gc[si][NG - 1];
+                ga[si][NG - 1] = p ? T_INF : ga[si][NG - 1];
+                ng[si] -= p ? 1 : 0;
+                if (!(sval(si) & (ng[si] > 0) & (ga[si][0] <= t))) break;
             }
         }
         if (cm) {
@@ -634,30 +639,26 @@ struct Sel {
         b.x = SEL_NONE;
         b.br = 0;
         uint32_t bi = 99u;
-        auto consider = [&](const Ent &x, uint32_t idx, int32_t L) {
-            const bool better = L > b.l || (L == b.l && (x.pa < b.a || (x.pa == b.a && idx < bi)));
-            if (better) {
-                b.l = L;
-                b.a = x.pa;
-                bi = idx;
-                b.s = x.s;
-                b.x = x.xo;
-                b.br = x.br;
-            }
+        auto consider = [&](const Ent &x, uint32_t idx, int32_t L, bool v) {
+            const bool better = v & ((L > b.l) | ((L == b.l) & ((x.pa < b.a) | ((x.pa == b.a) & (idx < bi)))));
+            b.l = better ? L : b.l;
+            b.a = better ? x.pa : b.a;
+            bi = better ? idx : bi;
+            b.s = better ? x.s : b.s;
+            b.x = better ? x.xo : b.x;
+            b.br = better ? x.br : b.br;
         };
-        if (pas) consider(P, (uint32_t)__builtin_ctz(pas), P.rt);
+        consider(P, pas ? (uint32_t)__builtin_ctz(pas) : 99u, P.rt, pas != 0u);
 #pragma unroll
-        for (int si = 0; si < NS; ++si)
-            if (sval(si)) consider(S[si], sidv[si], S[si].rp);
+        for (int si = 0; si < NS; ++si) consider(S[si], sidv[si], S[si].rp, sval(si));
 #pragma unroll
-        for (int a = 0; a < NA; ++a)
-            if (aval(a)) consider(A[a], aid[a], A[a].rp);
+        for (int a = 0; a < NA; ++a) consider(A[a], aid[a], A[a].rp, aval(a));
         if (cm) {
 #pragma unroll
             for (int c = 0; c < NC; ++c)
                 if (cval(c)) {
                     const ColdAct r = env.cold(c);
-                    consider(r.x, r.aid, r.x.rp);
+                    consider(r.x, r.aid, r.x.rp, true);
                 }
         }
         b.s = b.l >= WIN - 1 ? b.s : ((b.s & nib_upto(b.l)) | ~nib_upto(b.l));
@@ -670,11 +671,11 @@ struct Sel {
     template <class Env>
     MSIM_HD void reorg_ent(Env &env, Ent &x, bool is_p, uint32_t own, const SelBest &B, uint32_t pas)
     {
-        const bool same = !deep || x.br == B.br;
+        const bool same = (!deep) | (x.br == B.br);
         const int top = imin(x.rt, WIN - 1);
         const int d = same ? first_diff(x.s, B.s, top) : 0;
         const int32_t beyond = x.rt >= WIN ? x.rt - (WIN - 1) : 0;
-        const bool popb = beyond > 0 && (!same || d <= top || x.xo != B.x);
+        const bool popb = (beyond > 0) & ((!same) | (d <= top) | (x.xo != B.x));
         if (!same) SEL_HIT(11);
         if (is_p) {
             SEL_HIT(7);
@@ -841,7 +842,11 @@ struct Sel {
         merge(env);
         bpub = B.l;                   // main.cpp:171
         resolve(env);
-        if (fold_due(env, B.l)) fold(env);
+        // Folding is a change of representation only, so a lane may fold before it is due: the device
+        // folds every lane of a wave when any lane is due (one wave-uniform branch, and lanes that folded
+        // together are due again later, together).
+        const bool due = fold_due(env, B.l);
+        if (env.fold_vote(due)) fold(env, due);
         t_ = lmin(nbt_, earliest(env, t));  // main.cpp:176-182
         return true;
     }

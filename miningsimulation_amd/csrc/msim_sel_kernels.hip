@@ -31,6 +31,8 @@ struct SelDevEnv {
     __device__ __forceinline__ uint32_t get(int a, uint32_t k) const { return c[(a * M + (int)k) * TPB]; }
     __device__ __forceinline__ void add(int a, uint32_t k, uint32_t v) { atomicAdd(&c[(a * M + (int)k) * TPB], v); }
     __device__ __forceinline__ void set(int a, uint32_t k, uint32_t v) { c[(a * M + (int)k) * TPB] = v; }
+    // every lane of the wave folds when any lane is due (msim_sel.h step)
+    __device__ __forceinline__ bool fold_vote(bool due) const { return __builtin_amdgcn_ballot_w64(due) != 0ull; }
 };
 
 // The run's words (msim_sel_launch.h D1 layout), four at a time. The kernel loop issues the load of the
@@ -252,32 +254,26 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
         if (v[i]) atomicAdd((unsigned long long *)(a.retry_sums + (size_t)point * 6 * M + i), (unsigned long long)v[i]);
 }
 
+// One capacity class (2 hot active slots, 4 reveal groups, 2 in-flight blocks per hot slot, SEL_NC cold
+// slots) for every network: measured on the 360-point configs[3] sweep, a wider register class (3, 8, 3)
+// spilled and ran the whole sweep 2.1x slower than this one, which flagged no run.
 template <int M, int NS>
-static hipError_t launch_sel_ns(const SelArgs &a, uint32_t caps, hipStream_t s)
+static hipError_t launch_sel_ns(const SelArgs &a, hipStream_t s)
 {
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
-    const dim3 grid(a.nlist * wps);
-    if (caps == SEL_SMALL)
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC>), grid, dim3(TPB), 0, s, a);
-    else
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 3, 8, 3, SEL_NC>), grid, dim3(TPB), 0, s, a);
+    hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
     return hipGetLastError();
 }
 
 #if defined(MSIM_M)
 #define MSIM_CAT2(a, b) a##b
 #define MSIM_CAT(a, b) MSIM_CAT2(a, b)
-hipError_t MSIM_CAT(launch_sel_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, uint32_t caps, hipStream_t s)
+hipError_t MSIM_CAT(launch_sel_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, hipStream_t s)
 {
-    if (ns_class == 1) return launch_sel_ns<MSIM_M, 1>(a, caps, s);
+    if (ns_class == 1) return launch_sel_ns<MSIM_M, 1>(a, s);
 #if MSIM_M >= 2
-    // several selfish miners: the wide capacities in E1 as well
-    const uint32_t wps = (a.sn + TPB - 1) / TPB;
-    if (ns_class == 2)
-        hipLaunchKernelGGL((msim_sel_kernel<MSIM_M, 2, 3, 8, 3, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-    else
-        hipLaunchKernelGGL((msim_sel_kernel<MSIM_M, 4, 3, 8, 3, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-    return hipGetLastError();
+    if (ns_class == 2) return launch_sel_ns<MSIM_M, 2>(a, s);
+    return launch_sel_ns<MSIM_M, 4>(a, s);
 #else
     return hipErrorInvalidValue;
 #endif

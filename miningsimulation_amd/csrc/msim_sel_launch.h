@@ -25,13 +25,10 @@ namespace msim {
 
 constexpr uint32_t SEL_TILE = 32;  // words per (run, tile)
 
-// Capacity classes of E1 (hot active slots, reveal groups, in-flight blocks per hot active slot), all
-// backed by SEL_NC cold slots in global memory (msim_sel.h): SMALL = (2, 4, 2), LARGE = (3, 8, 3). A run
-// that exceeds them anyway is recomputed by E2, which costs a whole run-year on one lane, so E1 must
-// practically never flag.
-enum : uint32_t { SEL_SMALL = 0, SEL_LARGE = 1 };
+// Capacities of E1: 2 hot active slots, 4 reveal groups, 2 in-flight blocks per hot active slot, backed
+// by SEL_NC cold slots in global memory (msim_sel.h). A run that exceeds them anyway is recomputed by E2,
+// which costs a whole run-year on one lane, so E1 must practically never flag.
 constexpr int SEL_NC = 4;
-constexpr int64_t SEL_SMALL_MAX_PROP = 2000;  // ms: networks up to this propagation use SEL_SMALL
 
 // One network of a launch (a sweep point).
 struct SelParams {
@@ -130,11 +127,11 @@ inline SelLayout sel_layout_for(int64_t duration_ms, uint64_t n_runs, double bud
 
 hipError_t launch_word_draws(const WordArgs &a, hipStream_t s);
 hipError_t word_draws_blocks_per_cu(int *blocks);
-// E1 / E2 for miner count m, selfish class (1, 2, 4) and capacity class; dispatch in msim_common.hip.
-hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, uint32_t caps, hipStream_t s);
+// E1 / E2 for miner count m and selfish class (1, 2, 4); dispatch in msim_common.hip.
+hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
 #define MSIM_DECL_SEL(MM)                                                                               \
-    hipError_t launch_sel_m##MM(const SelArgs &a, uint32_t ns_class, uint32_t caps, hipStream_t s);     \
+    hipError_t launch_sel_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);                    \
     hipError_t launch_sel_retry_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);
 MSIM_FOR_EACH_M(MSIM_DECL_SEL)
 #undef MSIM_DECL_SEL

@@ -11,6 +11,8 @@ using namespace msim;
 
 namespace {
 
+uint32_t g_fold_every = 0;
+
 struct HostEnv {
     const int64_t *props;
     uint32_t c[4][MAXM];
@@ -21,6 +23,9 @@ struct HostEnv {
     void set(int a, uint32_t k, uint32_t v) { c[a][k] = v; }
     ColdAct cold(int i) const { return cs[i]; }
     void cold_put(int i, const ColdAct &r) { cs[i] = r; }
+    uint32_t fold_every;  // 0: fold when due; else also fold at every n-th event (as the device folds early)
+    uint32_t nev = 0;
+    bool fold_vote(bool due) { return due || (fold_every && ++nev % fold_every == 0); }
 };
 
 // Draws exactly as the reference's loop makes them (simulation.h:205-221), through the same packed
@@ -50,6 +55,7 @@ void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D,
     env.props = prop;
     memset(env.c, 0, sizeof(env.c));
     memset(env.cs, 0, sizeof(env.cs));
+    env.fold_every = g_fold_every;
     Sel<M, NS, NA, NG, NQ, NC> s;
     s.init((uint32_t)M, sids);
     s.run(env, src, D, o);
@@ -58,7 +64,7 @@ void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D,
 template <int M, int NS>
 void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
 {
-    // 0 / 3: the device's SMALL / LARGE classes (msim_sel_launch.h), 1: retry capacities,
+    // 0: the device E1 capacities (msim_sel_launch.h), 3: a wider register class, 1: retry capacities,
     // 2: one hot slot of everything (the cold paths run constantly), 4: no cold slots (error paths)
     if (caps == 0) run_one<M, NS, 2, 4, 2, 4>(prop, sids, src, D, o);
     else if (caps == 1) run_one<M, NS, 4, 16, 4, 6>(prop, sids, src, D, o);
@@ -68,6 +74,9 @@ void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src,
 }
 
 }  // namespace
+
+// Early folds in every later sel_run: 0 = only when due, n = also at every n-th event.
+extern "C" void sel_set_fold_every(uint32_t n) { g_fold_every = n; }
 
 // weights[m] summing to W, prop[m], selfish[m]; caps: see run_caps.
 extern "C" int sel_run(const uint64_t *weights, const int64_t *prop, const uint8_t *selfish, int m, uint64_t W,

@@ -18,6 +18,9 @@ D = 31_556_952_000
 @pytest.fixture(scope="module")
 def sel(native_tests):
     lib = ctypes.CDLL(native_tests["sel_host"])
+    lib.sel_set_fold_every.argtypes = [ctypes.c_uint32]
+    lib.sel_set_fold_every(0)
+    run_fold = lib.sel_set_fold_every
     lib.sel_run.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_uint64, ctypes.c_int64,
                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
@@ -36,6 +39,7 @@ def sel(native_tests):
         assert rc == 0
         return err.value, np.array([[f[k], s[k]] for k in range(m)], dtype=np.int64), bh.value
 
+    run.fold_every = run_fold
     return run
 
 
@@ -197,3 +201,29 @@ def test_edge_cases(sel, oracle):
     _check(sel, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, 0, 1, 2)
     _check(sel, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, 1, 1, 2)
     _check(sel, oracle, [10, 20, 30, 40], [1000] * 4, [False, False, False, True], 10**9, 11, 12)
+
+
+@pytest.mark.parametrize("every", [1, 3])
+def test_early_folds(sel, oracle, every):
+    """The device folds every lane of a wave when any lane is due (msim_sel.h step): folding before a lane
+    is due must not change any result. Fold at every event / every third event on top of the due ones."""
+    rng = random.Random(2024 + every)
+    sel.fold_every(every)
+    try:
+        for _ in range(30):
+            m = rng.randint(2, 12)
+            percs = _rand_percs(m, rng)
+            props = [rng.choice([100, 1000, 10_000, 30_000])] * m if rng.random() < 0.6 else \
+                [rng.choice([0, 100, 1000, 10_000, 30_000]) for _ in range(m)]
+            ns = rng.choice([0, 1, 1, 1, 2])
+            sidx = set(rng.sample(range(m), min(ns, m - 1)))
+            selfish = [k in sidx for k in range(m)]
+            caps = rng.choice([0, 2])
+            majority = sum(p for p, x in zip(percs, selfish) if x) > 50  # may exceed two deep branches
+            _check(sel, oracle, percs, props, selfish, rng.choice([10**9, 5 * 10**9]), rng.randrange(2**32),
+                   rng.randrange(2**32), caps=caps, allow_err=caps == 0 or (ns > 1 and majority))
+        for h, prop in ((40, 1000), (49, 30_000)):
+            _check(sel, oracle, [h, 59 - h, 12, 11, 8, 5, 3, 1, 1], [prop] * 9, [True] + [False] * 8, D, 1000, 1001,
+                   caps=1)
+    finally:
+        sel.fold_every(0)
