@@ -12,6 +12,7 @@
  *                            stats_total[j] += stats[j] aggregation (main.cpp:211-217)
  *   msim_stats            <- MinerStats {long blocks_found; double blocks_share; double stale_rate;}
  *                            (main.cpp:13-20), same field order and types
+ *   msim_run_multi        <- the same loop over several GPUs: shards + one RCCL all-reduce of msim_sums
  *   msim_launch           <- device-resident form of msim_run for hosts that own streams and an
  *                            RCCL communicator (multi-GPU: shard runs, all-reduce msim_sums)
  * Seeds: RunSimulation draws two 32-bit std::random_device values (main.cpp:131-134); run r of a
@@ -97,6 +98,14 @@ uint32_t msim_config_miner_count(const msim_config *cfg);
 int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, int device,
              msim_stats *out_sums, msim_sums *opt_sums, msim_run_record *opt_per_run, uint32_t *opt_best_height);
 
+/* Several GPUs of one node (the std::async loop of main.cpp:205-220 across devices): runs
+ * [run_begin, run_begin + n_runs) cut into contiguous shards, one per device in `devices` (NULL = devices
+ * 0 .. n_devices - 1), each through msim_launch on its own host thread and stream, then ONE ncclAllReduce
+ * (RCCL over xGMI, single-process communicator from ncclCommInitAll) of the integer msim_sums. The result
+ * is bit-identical to msim_run for every n_devices (out_sums from the fixed-point sums; opt_sums or NULL). */
+int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
+                   const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums);
+
 /* Device-resident launch on the current HIP device and the given hipStream_t (NULL = default).
  * d_sums: M msim_sums in device memory (overwritten). d_per_run / d_best_height: device buffers or NULL.
  * d_status: 2 uint32_t in device memory (required): [0] = runs that needed the retry kernel, [1] = runs
@@ -134,10 +143,16 @@ size_t msim_sweep_workspace_bytes(const msim_sweep *sweep, uint64_t runs_per_poi
 int msim_sweep_launch(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base,
                       void *d_sums, void *d_per_run, void *d_best_height, void *d_status, void *d_workspace,
                       size_t workspace_bytes, void *stream);
+uint32_t msim_sweep_point_count(const msim_sweep *sweep);
+uint32_t msim_sweep_miner_count(const msim_sweep *sweep);
 /* Host convenience: out_stats n_points * M (fixed-point sums converted), optional sums / records. */
 int msim_sweep_run(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base,
                    int device, msim_stats *out_stats, msim_sums *opt_sums, msim_run_record *opt_per_run,
                    uint32_t *opt_best_height);
+/* A sweep over several GPUs as msim_run_multi: every device runs every point on its shard of the runs,
+ * one RCCL all-reduce of the n_points * M sums; bit-identical to msim_sweep_run. */
+int msim_sweep_run_multi(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point, uint32_t seed_base,
+                         const int *devices, uint32_t n_devices, msim_stats *out_stats, msim_sums *opt_sums);
 
 /* Stage timing for measurement (bench.py): while enabled, every msim_launch records HIP events on its
  * stream around the whole launch and around each draw kernel (K1, the dominant kernel of the

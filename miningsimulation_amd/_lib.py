@@ -31,6 +31,10 @@ EXPORTED = (
     "msim_config_destroy",
     "msim_config_miner_count",
     "msim_run",
+    "msim_run_multi",
+    "msim_sweep_run_multi",
+    "msim_sweep_point_count",
+    "msim_sweep_miner_count",
     "msim_workspace_bytes",
     "msim_launch",
     "msim_device_log1p",
@@ -125,6 +129,16 @@ def _load() -> ctypes.CDLL:
     lib.msim_run.argtypes = [vp, u64, u64, u32, ctypes.c_int, ctypes.POINTER(MsimStats), ctypes.POINTER(MsimSums),
                              ctypes.POINTER(MsimRunRecord), ctypes.POINTER(u32)]
     lib.msim_run.restype = ctypes.c_int
+    lib.msim_run_multi.argtypes = [vp, u64, u64, u32, ctypes.POINTER(ctypes.c_int), u32, ctypes.POINTER(MsimStats),
+                                   ctypes.POINTER(MsimSums)]
+    lib.msim_run_multi.restype = ctypes.c_int
+    lib.msim_sweep_run_multi.argtypes = [vp, u64, u64, u32, ctypes.POINTER(ctypes.c_int), u32,
+                                         ctypes.POINTER(MsimStats), ctypes.POINTER(MsimSums)]
+    lib.msim_sweep_run_multi.restype = ctypes.c_int
+    lib.msim_sweep_point_count.argtypes = [vp]
+    lib.msim_sweep_point_count.restype = u32
+    lib.msim_sweep_miner_count.argtypes = [vp]
+    lib.msim_sweep_miner_count.restype = u32
     lib.msim_workspace_bytes.argtypes = [vp, u64]
     lib.msim_workspace_bytes.restype = sz
     lib.msim_launch.argtypes = [vp, u64, u64, u32, vp, vp, vp, vp, vp, sz, vp]

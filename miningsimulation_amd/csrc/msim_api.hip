@@ -779,12 +779,21 @@ int msim_device_picks(const msim_config *cfg, const uint64_t *d_uniform, int32_t
     return msim::launch_picks(t.pick, d_uniform, d_out_index, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
 }
 
+// A Q32.32 sum held as two limbs -> double with ONE rounding of the exact value (hi << 32) + lo, so the
+// result does not depend on how runs were split into workgroups, slices, launches or ranks (each split
+// moves value between the limbs but never changes the exact sum).
+static double fx_value(uint64_t hi, uint64_t lo)
+{
+    const unsigned __int128 v = ((unsigned __int128)hi << 32) + lo;
+    return (double)v * 0x1.0p-32;
+}
+
 void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out)
 {
     for (uint32_t k = 0; k < n; ++k) {
         out[k].blocks_found = sums[k].blocks_found;
-        out[k].blocks_share = (double)sums[k].share_hi + (double)sums[k].share_lo * 0x1.0p-32;
-        out[k].stale_rate = (double)sums[k].rate_hi + (double)sums[k].rate_lo * 0x1.0p-32;
+        out[k].blocks_share = fx_value(sums[k].share_hi, sums[k].share_lo);
+        out[k].stale_rate = fx_value(sums[k].rate_hi, sums[k].rate_lo);
     }
 }
 
@@ -916,6 +925,9 @@ void msim_sweep_destroy(msim_sweep *sw)
     for (const auto &d : sw->sdev) (void)hipFree(d.second);
     delete sw;
 }
+
+uint32_t msim_sweep_point_count(const msim_sweep *sw) { return sw ? (uint32_t)sw->pts.size() : 0u; }
+uint32_t msim_sweep_miner_count(const msim_sweep *sw) { return sw ? sw->m : 0u; }
 
 size_t msim_sweep_workspace_bytes(const msim_sweep *sw, uint64_t runs_per_point)
 {

@@ -1,0 +1,181 @@
+// msim_multi.hip — msim_run_multi / msim_sweep_run_multi: the reference's run loop (main.cpp:205-220) spread over several GPUs
+// of one node, combined with RCCL.
+//
+// The reference runs SIM_RUNS independent runs as std::async tasks and adds their MinerStats on the main
+// thread (main.cpp:209-217). Runs are independent and their seeds are a pure function of the run index,
+// so here the run range is cut into contiguous shards, one per device; each device's host thread runs its
+// shard through msim_launch (device-resident, its own stream), and the per-miner msim_sums (integers)
+// are combined by ONE ncclAllReduce over a single-process communicator (ncclCommInitAll: RCCL over xGMI
+// on MI355X). Integer sums make the result bit-identical to msim_run for every device count.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include <thread>
+#include <vector>
+
+#include "../../include/msim.h"
+
+namespace {
+
+// runs per msim_launch on one device (as msim_run: keeps every launch's workspace bounded)
+constexpr uint64_t MULTI_CHUNK = 1ull << 22;
+
+__global__ void add_sums_kernel(uint64_t *acc, const uint64_t *part, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) acc[i] += part[i];
+}
+
+__global__ void add_status_kernel(uint32_t *acc, const uint32_t *part)
+{
+    if (threadIdx.x < 2) acc[threadIdx.x] += part[threadIdx.x];
+}
+
+struct Shard {
+    int device;
+    uint64_t begin, n;
+    int rc = MSIM_OK;
+    uint64_t *d_acc = nullptr;   // [nv] sums of every chunk (the all-reduce operand)
+    uint32_t *d_stat = nullptr;  // [2] status of every chunk
+};
+
+// What one device launches for a chunk of runs: a config (msim_launch) or a sweep (msim_sweep_launch).
+struct Job {
+    const msim_config *cfg;
+    const msim_sweep *sweep;
+    uint32_t nv;  // int64 values of the sums: 6 * M (config) or 6 * M * points (sweep)
+    size_t ws_bytes(uint64_t n) const
+    {
+        return cfg ? msim_workspace_bytes(cfg, n) : msim_sweep_workspace_bytes(sweep, n);
+    }
+    int launch(uint64_t begin, uint64_t n, uint32_t seed_base, void *sums, void *status, void *ws, size_t wsb,
+               hipStream_t s) const
+    {
+        return cfg ? msim_launch(cfg, begin, n, seed_base, sums, nullptr, nullptr, status, ws, wsb, s)
+                   : msim_sweep_launch(sweep, begin, n, seed_base, sums, nullptr, nullptr, status, ws, wsb, s);
+    }
+};
+
+// One device: its shard in chunks, sums accumulated on the device, then the all-reduce.
+void run_shard(const Job &job, uint32_t seed_base, ncclComm_t comm, Shard &sh, hipStream_t *stream_out)
+{
+    if (hipSetDevice(sh.device) != hipSuccess) {
+        sh.rc = MSIM_E_HIP;
+        return;
+    }
+    hipStream_t s = nullptr;
+    void *ws = nullptr;
+    uint64_t *d_part = nullptr;
+    uint32_t *d_pst = nullptr;
+    const uint32_t nv = job.nv;
+    const uint64_t chunk = sh.n < MULTI_CHUNK ? sh.n : MULTI_CHUNK;
+    const size_t wsb = chunk ? job.ws_bytes(chunk) : 0;
+    if (hipStreamCreate(&s) != hipSuccess || hipMalloc(&sh.d_acc, nv * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&sh.d_stat, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&d_part, nv * sizeof(uint64_t)) != hipSuccess || hipMalloc(&d_pst, 2 * sizeof(uint32_t)) != hipSuccess ||
+        (wsb && hipMalloc(&ws, wsb) != hipSuccess) ||
+        hipMemsetAsync(sh.d_acc, 0, nv * sizeof(uint64_t), s) != hipSuccess ||
+        hipMemsetAsync(sh.d_stat, 0, 2 * sizeof(uint32_t), s) != hipSuccess) {
+        sh.rc = MSIM_E_HIP;
+    }
+    for (uint64_t off = 0; sh.rc == MSIM_OK && off < sh.n; off += chunk) {
+        const uint64_t cn = (sh.n - off) < chunk ? (sh.n - off) : chunk;
+        sh.rc = job.launch(sh.begin + off, cn, seed_base, d_part, d_pst, ws, wsb, s);
+        if (sh.rc) break;
+        hipLaunchKernelGGL(add_sums_kernel, dim3((nv + 255) / 256), dim3(256), 0, s, sh.d_acc, d_part, nv);
+        hipLaunchKernelGGL(add_status_kernel, dim3(1), dim3(64), 0, s, sh.d_stat, d_pst);
+        if (hipGetLastError() != hipSuccess) sh.rc = MSIM_E_HIP;
+    }
+    // Every rank takes part in the collectives, also after a local error (a rank that skipped them would
+    // leave the others waiting): a failed shard contributes zeros and reports its own error code.
+    if (ncclGroupStart() != ncclSuccess ||
+        ncclAllReduce(sh.d_acc, sh.d_acc, nv, ncclUint64, ncclSum, comm, s) != ncclSuccess ||
+        ncclAllReduce(sh.d_stat, sh.d_stat, 2, ncclUint32, ncclSum, comm, s) != ncclSuccess ||
+        ncclGroupEnd() != ncclSuccess)
+        sh.rc = sh.rc ? sh.rc : MSIM_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) sh.rc = sh.rc ? sh.rc : MSIM_E_HIP;
+    (void)hipFree(ws);
+    (void)hipFree(d_part);
+    (void)hipFree(d_pst);
+    *stream_out = s;
+}
+
+// Shards [run_begin, run_begin + n_runs) over the devices, runs them, all-reduces; acc = reduced sums.
+int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, const int *devices,
+            uint32_t n_devices, std::vector<uint64_t> &acc)
+{
+    std::vector<int> devs(n_devices);
+    for (uint32_t g = 0; g < n_devices; ++g) devs[g] = devices ? devices[g] : (int)g;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return MSIM_E_HIP;
+    for (int d : devs)
+        if (d < 0 || d >= count) return MSIM_E_INVALID;
+    std::vector<ncclComm_t> comms(n_devices);
+    if (ncclCommInitAll(comms.data(), (int)n_devices, devs.data()) != ncclSuccess) return MSIM_E_HIP;
+    // contiguous shards, as distributed.shard: the first n_runs % n_devices shards take one run more
+    std::vector<Shard> sh(n_devices);
+    const uint64_t base = n_runs / n_devices, rem = n_runs % n_devices;
+    for (uint32_t g = 0; g < n_devices; ++g) {
+        sh[g].device = devs[g];
+        sh[g].begin = run_begin + g * base + (g < rem ? g : rem);
+        sh[g].n = base + (g < rem ? 1 : 0);
+    }
+    std::vector<hipStream_t> streams(n_devices, nullptr);
+    std::vector<std::thread> th;
+    for (uint32_t g = 0; g < n_devices; ++g)
+        th.emplace_back(run_shard, std::cref(job), seed_base, comms[g], std::ref(sh[g]), &streams[g]);
+    for (auto &t : th) t.join();
+    int rc = MSIM_OK;
+    for (const auto &x : sh)
+        if (x.rc) rc = rc ? rc : x.rc;
+    acc.assign(job.nv, 0);
+    uint32_t st[2] = {0, 0};
+    if (rc == MSIM_OK) {  // every rank holds the reduced sums: read the first device's
+        if (hipSetDevice(sh[0].device) != hipSuccess ||
+            hipMemcpy(acc.data(), sh[0].d_acc, acc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(st, sh[0].d_stat, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = MSIM_E_HIP;
+        else if (st[1] != 0)
+            rc = MSIM_E_CAPACITY;
+    }
+    for (uint32_t g = 0; g < n_devices; ++g) {
+        (void)hipSetDevice(sh[g].device);
+        (void)hipFree(sh[g].d_acc);
+        (void)hipFree(sh[g].d_stat);
+        if (streams[g]) (void)hipStreamDestroy(streams[g]);
+        (void)ncclCommDestroy(comms[g]);
+    }
+    return rc;
+}
+
+}  // namespace
+
+extern "C" int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
+                              const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums)
+{
+    if (!cfg || !out_sums || n_runs == 0 || n_devices == 0 || n_devices > 64) return MSIM_E_INVALID;
+    const uint32_t m = msim_config_miner_count(cfg);
+    std::vector<uint64_t> acc;
+    const int rc = run_job(Job{cfg, nullptr, 6 * m}, run_begin, n_runs, seed_base, devices, n_devices, acc);
+    if (rc) return rc;
+    const msim_sums *fs = (const msim_sums *)acc.data();
+    if (opt_sums) memcpy(opt_sums, fs, sizeof(msim_sums) * m);
+    msim_sums_to_stats(fs, m, out_sums);
+    return MSIM_OK;
+}
+
+extern "C" int msim_sweep_run_multi(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point,
+                                    uint32_t seed_base, const int *devices, uint32_t n_devices, msim_stats *out_stats,
+                                    msim_sums *opt_sums)
+{
+    if (!sweep || !out_stats || runs_per_point == 0 || n_devices == 0 || n_devices > 64) return MSIM_E_INVALID;
+    const uint32_t nv = 6 * msim_sweep_miner_count(sweep) * msim_sweep_point_count(sweep);
+    std::vector<uint64_t> acc;
+    const int rc = run_job(Job{nullptr, sweep, nv}, run_begin, runs_per_point, seed_base, devices, n_devices, acc);
+    if (rc) return rc;
+    const msim_sums *fs = (const msim_sums *)acc.data();
+    if (opt_sums) memcpy(opt_sums, fs, sizeof(uint64_t) * nv);
+    msim_sums_to_stats(fs, nv / 6, out_stats);
+    return MSIM_OK;
+}

@@ -56,11 +56,16 @@ def allreduce_sums(local_rows, device=None):
     return t.cpu().tolist()
 
 
-def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=None,
-                launch: Optional[Callable] = None):
-    """GPU path: this rank's shard through msim_launch on the current device, then one RCCL all-reduce.
+MAX_LAUNCH_RUNS = 1 << 26  # msim_launch's per-call limit (msim_api.hip); larger shards run in chunks
 
-    Returns the global [M, 6] int64 sums as a device tensor (identical on every rank)."""
+
+def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=None,
+                launch: Optional[Callable] = None, device=None):
+    """This rank's shard through msim_launch on the current device, then one all-reduce (RCCL on GPUs).
+
+    Returns the global [M, 6] int64 sums as a tensor on `device` (identical on every rank). `launch`
+    replaces sim.launch (same signature, workspace None) so that the partition, chunking, status check and
+    all-reduce can be exercised on CPU ranks with a gloo group (tests/test_distributed.py)."""
     import torch
     import torch.distributed as dist
 
@@ -68,12 +73,20 @@ def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=No
     rank = dist.get_rank() if dist.is_initialized() else 0
     begin, n = shard(n_total, world, rank)
     m = len(sim.miners)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
     status = torch.zeros(2, dtype=torch.int32, device=dev)
-    if n:
-        ws = torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev)
-        (launch or sim.launch)(n, run_begin + begin, seed_base, sums, ws, status, stream=stream)
+    part = torch.zeros_like(sums)
+    pst = torch.zeros_like(status)
+    chunk = min(n, MAX_LAUNCH_RUNS)
+    ws = None
+    if n and launch is None:
+        ws = torch.empty(sim.workspace_bytes(chunk), dtype=torch.uint8, device=dev)
+    for off in range(0, n, max(chunk, 1)):
+        cn = min(chunk, n - off)
+        (launch or sim.launch)(cn, run_begin + begin + off, seed_base, part, ws, pst, stream=stream)
+        sums += part
+        status += pst
     if world > 1:
         dist.all_reduce(sums)
         dist.all_reduce(status)

@@ -166,6 +166,22 @@ class Simulation:
             res.best_height = np.ctypeslib.as_array(bh).copy()
         return res
 
+    def run_multi(self, n_runs: int, run_begin: int = 0, seed_base: int = DEFAULT_SEED_BASE,
+                  devices: Sequence[int] = (0,)) -> SimulationResult:
+        """msim_run_multi: the runs sharded over `devices` (one host thread each) and combined with one RCCL
+        all-reduce of the integer sums; bit-identical to run() for any device list."""
+        m = len(self.miners)
+        stats = (MsimStats * m)()
+        sums = (MsimSums * m)()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        check(lib.msim_run_multi(self._h, run_begin, n_runs, seed_base & 0xFFFFFFFF, devs, len(devices), stats, sums),
+              "msim_run_multi")
+        return SimulationResult(
+            stats_total=[MinerStats(s.blocks_found, s.blocks_share, s.stale_rate) for s in stats],
+            sums=list(sums),
+            n_runs=n_runs,
+        )
+
     def pipeline_info(self, n_runs: int) -> dict:
         """How msim_launch executes n_runs on the current device (msim_pipeline_info)."""
         pl = _lib.MsimPipelineLayout()
@@ -233,6 +249,22 @@ class Sweep:
             lib.msim_sweep_destroy(h)
             self._h = None
 
+    def run_multi(self, runs_per_point: int, run_begin: int = 0, seed_base: int = DEFAULT_SEED_BASE,
+                  devices: Sequence[int] = (0,)) -> List[SimulationResult]:
+        """msim_sweep_run_multi: every device runs every point on its shard of the runs, one RCCL all-reduce;
+        bit-identical to run()'s sums for any device list."""
+        n, m = len(self.sims), self.m
+        stats = (MsimStats * (n * m))()
+        sums = (MsimSums * (n * m))()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        check(lib.msim_sweep_run_multi(self._h, run_begin, runs_per_point, seed_base & 0xFFFFFFFF, devs, len(devices),
+                                       stats, sums), "msim_sweep_run_multi")
+        return [SimulationResult(
+            stats_total=[MinerStats(s.blocks_found, s.blocks_share, s.stale_rate) for s in stats[p * m:(p + 1) * m]],
+            sums=list(sums[p * m:(p + 1) * m]),
+            n_runs=runs_per_point,
+        ) for p in range(n)]
+
     def run(self, runs_per_point: int, run_begin: int = 0, seed_base: int = DEFAULT_SEED_BASE, device: int = 0,
             per_run: bool = False) -> List[SimulationResult]:
         n, m = len(self.sims), self.m
@@ -287,11 +319,14 @@ def timing_read() -> dict:
 
 
 def sums_to_stats(sums_rows: Iterable[Sequence[int]]) -> List[MinerStats]:
-    """Fixed-point msim_sums rows ([found, stale, share_hi, share_lo, rate_hi, rate_lo]) -> MinerStats."""
+    """Fixed-point msim_sums rows ([found, stale, share_hi, share_lo, rate_hi, rate_lo]) -> MinerStats.
+
+    Each Q32.32 sum is converted with one rounding of its exact value (hi << 32) + lo (as
+    msim_sums_to_stats), so the result is the same for every split of the runs into launches or ranks."""
     out = []
     for r in sums_rows:
         found, _stale, sh, sl, rh, rl = (int(x) for x in r)
-        out.append(MinerStats(found, float(sh) + float(sl) * 2.0 ** -32, float(rh) + float(rl) * 2.0 ** -32))
+        out.append(MinerStats(found, float((sh << 32) + sl) * 2.0 ** -32, float((rh << 32) + rl) * 2.0 ** -32))
     return out
 
 

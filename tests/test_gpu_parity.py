@@ -257,7 +257,7 @@ def test_host_dropin_driver(msim):
     # (bytes, then decode: text mode's universal newlines would turn that "\r" into "\n")
     raw = subprocess.run([exe, "1", "1000"], capture_output=True, check=True).stdout
     out = raw.decode().rstrip("\n").split("\n")
-    assert out[0] == "Running 32768 simulations in parallel using 1 GPU(s)."
+    assert out[0] == "Running 32768 simulations in parallel using 1 threads."  # main.cpp:201's format
     assert out[1] == "\r100% progress.."
     assert out[2] == "After running 32768 simulations for 365d each, on average:"
     miners = msim.setup_miners(1000)
@@ -278,3 +278,41 @@ def test_host_dropin_driver_large_network(msim):
     assert len(out) == 3 + 1026
     assert out[3].startswith("  - Miner 0 (30% of network hashrate) found ")
     assert out[5].startswith("  - Miner 2 (0.0400391% of network hashrate) found ")
+
+
+def test_host_dropin_driver_sweep(msim, tmp_path):
+    """host/msim_main's sweep surface: a 3-point JSON network list (one sweep launch, msim_sweep_run_multi)
+    printed as JSON lines, and a 3-point --grid printed as main.cpp:224-234 reports, both equal to the
+    Python Sweep path's fixed-point sums for the same runs."""
+    import json
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(GOLD), "..", "host", "msim_main")
+    pts = [msim.setup_miners(1000, selfish_perc=40), msim.setup_miners(10_000, selfish_perc=25),
+           msim.setup_miners(100)]
+    spec = {"runs": 1024, "seed_base": 1000,
+            "points": [{"miners": [{"id": m.id, "perc": m.perc, "propagation_ms": m.propagation_ms,
+                                    "selfish": m.is_selfish} for m in p]} for p in pts]}
+    f = tmp_path / "sweep.json"
+    f.write_text(json.dumps(spec))
+    raw = subprocess.run([exe, "--sweep", str(f), "--json"], capture_output=True, check=True).stdout.decode()
+    lines = [json.loads(x) for x in raw.strip().split("\n")]
+    assert len(lines) == 3
+    want = msim.Sweep(pts).run(1024, 0, 1000, 0)
+    for p, (line, res) in enumerate(zip(lines, want)):
+        assert line["point"] == p and line["runs"] == 1024
+        for m, w in zip(line["miners"], res.stats_total):
+            assert m["blocks_share"] == w.blocks_share / 1024
+            assert m["stale_rate"] == w.stale_rate / 1024
+            assert m["blocks_found"] == w.blocks_found / 1024
+    # the grid form: selfish share x propagation over SetupMiners, text reports
+    raw = subprocess.run([exe, "--grid", "10,45:1000", "--runs", "512"], capture_output=True, check=True).stdout
+    out = raw.decode().rstrip("\n").split("\n")
+    grid = [msim.setup_miners(1000, selfish_perc=10), msim.setup_miners(1000, selfish_perc=45)]
+    res = msim.Sweep(grid).run(512, 0, 1000, 0)
+    want = []
+    for p, (g, r) in enumerate(zip(grid, res)):
+        want.append(f"Point {p + 1} of 2:")
+        rows = [[s.blocks_found, s.stale_blocks, s.share_hi, s.share_lo, s.rate_hi, s.rate_lo] for s in r.sums]
+        want += msim.report(g, msim.sums_to_stats(rows), 512).splitlines()
+    assert out == want

@@ -131,6 +131,9 @@ def test_gpu_wide_equals_narrow_pipeline(msim, monkeypatch):
         assert a.blocks_found == b.blocks_found and a.stale_blocks == b.stale_blocks
         assert (a.share_hi << 32) + a.share_lo == (b.share_hi << 32) + b.share_lo
         assert (a.rate_hi << 32) + a.rate_lo == (b.rate_hi << 32) + b.rate_lo
+        # the reported f64 statistics are bit-identical (one rounding of the exact limb sum)
+        x, y = narrow.stats_total[k], wide.stats_total[k]
+        assert x.blocks_share == y.blocks_share and x.stale_rate == y.stale_rate
 
 
 def test_gpu_wide_c5_full_slice_invariants(msim):
@@ -161,3 +164,10 @@ def test_gpu_wide_sharding_is_exact(msim):
         assert x.blocks_found == y.blocks_found + z.blocks_found
         assert x.stale_blocks == y.stale_blocks + z.stale_blocks
         assert (x.share_hi << 32) + x.share_lo == (y.share_hi << 32) + y.share_lo + (z.share_hi << 32) + z.share_lo
+    # the two halves' limbs added as a caller (or an all-reduce) would, then converted: bit for bit equal
+    rows = [[y.blocks_found + z.blocks_found, y.stale_blocks + z.stale_blocks, y.share_hi + z.share_hi,
+             y.share_lo + z.share_lo, y.rate_hi + z.rate_hi, y.rate_lo + z.rate_lo]
+            for y, z in zip(a.sums, b.sums)]
+    for s_whole, s_halves in zip(whole.stats_total, msim.sums_to_stats(rows)):
+        assert s_whole.blocks_share == s_halves.blocks_share
+        assert s_whole.stale_rate == s_halves.stale_rate
