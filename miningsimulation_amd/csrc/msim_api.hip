@@ -357,6 +357,10 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
     sp->uniform_prop = 1;
     for (uint32_t k = 1; k < n; ++k)
         if (miners[k].propagation_ms != miners[0].propagation_ms) sp->uniform_prop = 0;
+    sp->macro = sp->ns == 1 ? 1u : 0u;
+    for (uint32_t k = 0; k < n; ++k)
+        if (miners[k].propagation_ms < 1) sp->macro = 0;
+    if (getenv("MSIM_SEL_NO_MACRO")) sp->macro = 0;  // A/B switch: the entity engine for every find
 }
 
 struct SelGroupDev {

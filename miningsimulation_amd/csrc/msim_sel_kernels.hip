@@ -5,6 +5,7 @@
 #include "msim_kernels.h"
 #include "msim_reduce.h"
 #include "msim_sel_launch.h"
+#include "msim_selm.h"
 
 namespace msim {
 
@@ -84,7 +85,8 @@ struct SelWordSrc {
             hp = false;
         }
     }
-    __device__ __forceinline__ bool next(uint32_t &I, uint32_t &k)
+    // The next block's (interval, finder) without consuming it (the macro form looks one find ahead).
+    __device__ __forceinline__ bool peek(uint32_t &I, uint32_t &k)
     {
         if (b >= nb) return false;
         if (left == 0) {
@@ -98,17 +100,26 @@ struct SelWordSrc {
             hn = false;
         }
         const uint32_t w = c0;
-        c0 = c1;
-        c1 = c2;
-        c2 = c3;
-        --left;
-        ++b;
         I = w >> 7;
         const uint32_t q = w & 127u;
         uint32_t f = 0;
 #pragma unroll
         for (int j = 0; j < M; ++j) f += cc[j] <= q ? 1u : 0u;
         k = f;  // >= m: PickFinder falls through (simulation.h:220)
+        return true;
+    }
+    __device__ __forceinline__ void pop()
+    {
+        c0 = c1;
+        c1 = c2;
+        c2 = c3;
+        --left;
+        ++b;
+    }
+    __device__ __forceinline__ bool next(uint32_t &I, uint32_t &k)
+    {
+        if (!peek(I, k)) return false;
+        pop();
         return true;
     }
 };
@@ -118,8 +129,16 @@ struct SelWordSrc {
 struct SelRngSrc {
     Rng ri, rp;
     const SelParams *P;
+    uint32_t hI, hk;  // a block drawn by peek() and not yet consumed
+    bool held;
     __device__ bool next(uint32_t &I, uint32_t &k)
     {
+        if (held) {
+            held = false;
+            I = hI;
+            k = hk;
+            return true;
+        }
         I = (uint32_t)next_interval(ri);
         const uint64_t u = rng_next(rp);
         const uint64_t p1 = __umul64hi(u, (uint64_t)P->W);
@@ -129,6 +148,17 @@ struct SelRngSrc {
         k = f;
         return true;
     }
+    __device__ bool peek(uint32_t &I, uint32_t &k)
+    {
+        if (!held) {
+            next(hI, hk);
+            held = true;
+        }
+        I = hI;
+        k = hk;
+        return true;
+    }
+    __device__ void pop() { held = false; }
 };
 
 template <int M>
@@ -150,6 +180,112 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
         v[6 * k + 4] = rfx >> 32;
         v[6 * k + 5] = rfx & 0xFFFFFFFFull;
     }
+}
+
+// The mixed schedule of a network with one selfish miner (msim_selm.h): every lane runs the settled-state
+// form until one of its finds needs the entity engine, then waits; the wave switches to engine steps when
+// SEL_XTH lanes wait (or no lane is left in the settled form) and back when fewer than SEL_XLO lanes are in
+// the engine, so both phases run with most lanes active. Lane modes: 0 settled form, 1 waiting for the
+// engine, 2 in the engine, 3 done. The schedule only decides the order in which lanes advance: each lane's
+// result is that of its own sequence of transitions (tests/native/sel_host.cpp runs one lane alone).
+#ifndef SEL_XTH
+#define SEL_XTH 16
+#endif
+#ifndef SEL_XLO
+#define SEL_XLO 4
+#endif
+template <int M, class Env, class Src, class S>
+__device__ __forceinline__ void sel_mixed(Env &env, Src &src, S &s, const SelParams *P, int64_t D, SelOut &o)
+{
+    SelMacro<M> mc;
+    // A lane that finishes parks its counters in its own LDS counter rows (C_F, C_S) so that no result
+    // register stays live across the loop of the others.
+    uint32_t bh = 0, err = 0;
+    auto park = [&](const SelOut &r) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            env.set(C_F, (uint32_t)k, r.found[k]);
+            env.set(C_S, (uint32_t)k, r.stale[k]);
+        }
+        bh = r.best_height;
+        err = r.err;
+    };
+    const uint32_t sid = P->sids[0];
+    const int64_t ps = P->prop[sid];
+    const bool mac = P->macro != 0u;  // wave-uniform (one point per workgroup)
+    int mode = 0;
+    if (!mac) {  // the entity engine for every find
+        s.begin(src);
+        mode = 2;
+    } else if (!mc.begin(src)) {
+        err = SERR_DRAWS;
+        mode = 3;
+    } else if (mc.T >= D) {
+        SelOut r;
+        mc.finish(env, sid, r);
+        park(r);
+        mode = 3;
+    }
+    for (;;) {
+        const uint64_t bm = __builtin_amdgcn_ballot_w64(mode == 0);
+        const uint64_t be = __builtin_amdgcn_ballot_w64(mode == 1 || mode == 2);
+        if ((bm | be) == 0ull) break;
+        if (be != 0ull && (__builtin_popcountll(be) >= SEL_XTH || bm == 0ull)) {
+            if (mode == 1) {
+                mc.to_exact(env, s, P->m, P->sids);
+                mode = 2;
+            }
+            for (;;) {
+                if (mode == 2) {
+                    src.prefetch();
+                    const bool live = s.step(env, src, D);
+                    src.settle();
+                    if (!live) {
+                        SelOut r;
+                        s.finish(env, D, r);
+                        park(r);
+                        mode = 3;
+                    } else if (mac && mc.take_back(env, s, sid)) {
+                        if (mc.T >= D) {
+                            SelOut r;
+                            mc.finish(env, sid, r);
+                            park(r);
+                            mode = 3;
+                        } else {
+                            mode = 0;
+                        }
+                    }
+                }
+                const uint64_t b2 = __builtin_amdgcn_ballot_w64(mode == 2);
+                if (__builtin_popcountll(b2) < SEL_XLO && (b2 == 0ull || __builtin_amdgcn_ballot_w64(mode == 0) != 0ull)) break;
+            }
+        } else {
+            for (;;) {
+                if (mode == 0) {
+                    src.prefetch();  // consumed at a later refill (peek settles only when it must)
+                    const int r = mc.step(env, src, D, sid, ps);
+                    if (r == 2) {
+                        SelOut q;
+                        mc.finish(env, sid, q);
+                        park(q);
+                        mode = 3;
+                    } else if (r == 1) {
+                        mode = 1;
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
+                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 1 || mode == 2)) >= SEL_XTH)
+                    break;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        o.found[k] = env.get(C_F, (uint32_t)k);
+        o.stale[k] = env.get(C_S, (uint32_t)k);
+    }
+    o.best_height = bh;
+    o.err = err;
 }
 
 // E1: one lane per (point, run of the slice); workgroups never straddle points.
@@ -187,14 +323,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         if (a.force_retry) {
             o.err = SERR_CAP;
         } else {
-            s.begin(src);
-            for (;;) {
-                src.prefetch();
-                const bool live = s.step(env, src, D);
-                src.settle();
-                if (!live) break;
+            if constexpr (NS == 1) {
+                sel_mixed<M>(env, src, s, P, D, o);
+            } else {
+                s.begin(src);
+                for (;;) {
+                    src.prefetch();
+                    const bool live = s.step(env, src, D);
+                    src.settle();
+                    if (!live) break;
+                }
+                s.finish(env, D, o);
             }
-            s.finish(env, D, o);
         }
         if (o.err) {
             const uint32_t pos = atomicAdd(a.counts, 1u);

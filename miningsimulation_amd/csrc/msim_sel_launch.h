@@ -45,7 +45,7 @@ struct SelParams {
     // and ccum = cumulative percentages (first k with cum_k > q, simulation.h:217-218); weighted words
     // carry the finder and ccum[k] = k + 1. Unused entries 0xFFFFFFFF; a result >= m falls through.
     uint32_t ccum[MAXM];
-    uint32_t pad2;
+    uint32_t macro;      // 1: one selfish miner, every propagation >= 1 ms (the settled form applies, msim_selm.h)
 };
 
 struct WordArgs {

@@ -1,0 +1,247 @@
+// msim_selm.h — the settled-state ("macro") form of a run with ONE selfish miner, exact, and its hand-over
+// to and from the entity engine (msim_sel.h).
+//
+// Why. With one selfish miner (simulation.h:55) and every propagation delay >= 1 ms, a find whose
+// consequences (the honest block's arrival at T + prop_k, the selfish reveal it triggers, arriving
+// prop_s later — simulation.h:149-174, main.cpp:164-167) are all over before the next find leaves
+// the network in one of few SETTLED states, and the whole event sequence of that find collapses into one
+// transition of a small Markov chain (the 2013 paper's state machine with gamma = 0, as the reference
+// implements it):
+//   F   the common prefix (every miner's chain agrees up to height F, all published),
+//   h   the length of a published tie fork above F: the honest miners' branch (h honest blocks) and the
+//       selfish miner's published branch (h selfish blocks); the honest branch arrived first, so it is
+//       BestChain's pick (main.cpp:75 first-seen) and the honest miners stay on it,
+//   w   the selfish miner's withheld blocks on top of its branch (SelfishBlocks, simulation.h:105-115).
+// A settled state always has the selfish published branch as long as the honest one, so FoundBlock's
+// 1-block-race case (simulation.h:66) never applies. Transitions for a find by miner k:
+//   selfish                       w += 1                                    (simulation.h:71)
+//   honest, w == 0                the honest branch (+ k's block) wins: F += h + 1; the selfish miner's h
+//                                 tie blocks are stale (MaybeReorg, simulation.h:124-142)
+//   honest, w == 1 or w >= 3      one block is revealed (lead w - 1, simulation.h:160-163) and ties the
+//                                 new honest block: h += 1, w -= 1
+//   honest, w == 2                lead 1: everything is revealed (simulation.h:166-168) and the selfish
+//                                 branch (h + 2 blocks) wins: F += h + 2; the honest branch is stale
+// The transition is exact when the find is selfish (nothing is published) or when the next find comes
+// strictly after prop_k (+ prop_s if w > 0) and that settle time is before the end of the run D; every
+// other find is handed to the entity engine, which runs the reference's event loop until the network is
+// quiet again (a common published chain, only withheld blocks on top) and hands the run back.
+//
+// Counters: found[k] is counted provisionally at every find (the LDS C_F array); blocks that later leave
+// the best chain (stale honest branches: st[], stale selfish tie blocks: sst; the honest branch's
+// composition is kept as 16-bit counts per miner in pend[]) are subtracted when they are flushed.
+#pragma once
+#include "msim_sel.h"
+
+namespace msim {
+
+template <int M>
+struct SelMacro {
+    static constexpr int NPW = (M + 1) / 2;
+    int64_t T;             // time of the pending find
+    uint32_t k;            // its finder
+    uint32_t F, h, w;      // settled state (see above)
+    uint32_t pend[NPW];    // honest branch: blocks per honest miner, 16 bits each
+    uint32_t st[M];        // honest stale blocks not yet flushed to C_S
+    uint32_t sst;          // selfish stale blocks not yet flushed
+
+    MSIM_HD uint32_t pend_of(int j) const { return (pend[j >> 1] >> (16 * (j & 1))) & 0xFFFFu; }
+
+    // Start of a run (main.cpp:138, 149): the first find, at the first interval; genesis is the prefix.
+    template <class Src>
+    MSIM_HD bool begin(Src &src)
+    {
+        F = 0;
+        h = 0;
+        w = 0;
+        sst = 0;
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) pend[i] = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) st[j] = 0;
+        uint32_t I = 0;
+        if (!src.peek(I, k)) return false;
+        src.pop();
+        T = (int64_t)I;
+        return true;
+    }
+
+    // One find. Returns 0 (next find pending), 1 (this find needs the entity engine), 2 (run over: the
+    // next find is at or after D).
+    template <class Env, class Src>
+    MSIM_HD int step(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
+    {
+        uint32_t I = 0, kn = 0;
+        const bool have = src.peek(I, kn);
+        const bool is_s = k == sid;
+        const int64_t thr = is_s ? 0 : env.prop(k) + (w != 0u ? ps : 0);
+        const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (is_s | (((int64_t)I > thr) & (T + thr < D)));
+        if (!ok) return 1;
+        const bool hon = !is_s;
+        const bool res = hon & (w == 0u);     // the honest branch wins (h == 0: a plain honest block)
+        const bool swin = hon & (w == 2u);    // the selfish branch wins
+        const bool tie = hon & !res & !swin;  // one more tied block each
+        // k's block joins the honest branch (a resolving branch is cleared below)
+        const uint32_t inc = hon ? 1u << (16 * (k & 1u)) : 0u;
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) pend[i] += (k >> 1) == (uint32_t)i ? inc : 0u;
+#pragma unroll
+        for (int j = 0; j < M; ++j) st[j] += swin ? pend_of(j) : 0u;
+        sst += res ? h : 0u;
+        F += res ? h + 1u : (swin ? h + 2u : 0u);
+        h = (res | swin) ? 0u : h + (tie ? 1u : 0u);
+        w = is_s ? w + 1u : ((res | swin) ? 0u : w - 1u);
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) pend[i] = (res | swin) ? 0u : pend[i];
+        env.add(C_F, k, 1u);
+        src.pop();
+        T += (int64_t)I;
+        k = kn;
+        return T < D ? 0 : 2;
+    }
+
+    template <class Env>
+    MSIM_HD void flush_stale(Env &env, uint32_t sid)
+    {
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            if (st[j]) {
+                env.add(C_S, (uint32_t)j, st[j]);
+                env.add(C_F, (uint32_t)j, 0u - st[j]);
+                st[j] = 0;
+            }
+        if (sst) {
+            env.add(C_S, sid, sst);
+            env.add(C_F, sid, 0u - sst);
+            sst = 0;
+        }
+    }
+
+    // main.cpp:185-189 from a settled state: the honest branch is the best chain (first seen), the selfish
+    // tie blocks and withheld blocks are not in it.
+    template <class Env>
+    MSIM_HD void finish(Env &env, uint32_t sid, SelOut &out)
+    {
+        flush_stale(env, sid);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            out.found[j] = env.get(C_F, (uint32_t)j) - ((uint32_t)j == sid ? h + w : 0u);
+            out.stale[j] = env.get(C_S, (uint32_t)j);
+        }
+        out.best_height = F + h;
+        out.err = 0;
+    }
+
+    // Hand the run to the entity engine at the pending find. The tie fork becomes the engine's two-branch
+    // ("deep") form: window base F + h + 1, honest branch counts in C_A, the selfish branch in C_B. Tip
+    // arrivals only order chains of equal length (main.cpp:75); every settled tip arrived before T and
+    // every later block arrives after T, so T - 2 (honest tip) < T - 1 (selfish published tip) keeps
+    // every comparison the reference makes.
+    template <class Env, int NS, int NA, int NG, int NQ, int NC>
+    MSIM_HD void to_exact(Env &env, Sel<M, NS, NA, NG, NQ, NC> &s, uint32_t m, const uint32_t *sids)
+    {
+        const uint32_t sid = sids[0];
+        flush_stale(env, sid);
+        s.init(m, sids);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const uint32_t p = pend_of(j);
+            if (p) {
+                env.add(C_F, (uint32_t)j, 0u - p);
+                env.set(C_A, (uint32_t)j, p);
+            }
+        }
+        env.add(C_F, sid, 0u - (h + w));
+        if (h) env.set(C_B, sid, h);
+        s.wb = F + h + 1u;
+        s.deep = h != 0u;
+        s.P.pa = h ? T - 2 : T - 1;
+        Ent &X = s.S[0];
+        X.pa = T - 1;
+        X.br = h ? 1u : 0u;
+        X.rp = -1;
+        X.rt = (int32_t)w - 1;
+        const int top = imin((int)w, WIN) - 1;
+        X.s = (nib_upto(top) & (0x1111111111111111ull * (uint64_t)sid)) | ~nib_upto(top);
+        X.xo = w > (uint32_t)WIN ? sid : SEL_NONE;
+        s.w[0] = (int32_t)w;
+        s.bpub = -1;
+        s.t_ = T;
+        s.nbt_ = T;
+        s.kn_ = k;
+    }
+
+    // Take the run back from the engine when its state is settled (see above): nothing in flight, every
+    // honest miner in the passive class on a published chain, the selfish miner on a published chain of the
+    // same length plus withheld blocks, and either one common chain (a quiet network) or a tie fork whose
+    // honest branch holds only honest blocks, whose selfish branch holds only the selfish miner's blocks,
+    // and whose honest tip wins BestChain's tie-break (main.cpp:75). The fork's blocks may sit in the
+    // window or, during a two-branch episode, partly in the deep-branch counters. Returns false (and
+    // changes nothing) otherwise.
+    template <class Env, int NS, int NA, int NG, int NQ, int NC>
+    MSIM_HD bool take_back(Env &env, Sel<M, NS, NA, NG, NQ, NC> &s, uint32_t sid)
+    {
+        const Ent &P = s.P, &X = s.S[0];
+        const bool calm = ((s.av | s.cm | s.am) == 0u) & (s.ng[0] == 0) & (s.err == 0u) & (s.t_ == s.nbt_);
+        const bool shape = (P.rp == P.rt) & (P.rt < WIN) & (X.rp == P.rt) & (s.w[0] == X.rt - X.rp);
+        if (!(calm & shape)) return false;
+        // withheld blocks: the selfish miner's own (window part and implicit run)
+        const int wtop = imin(X.rt, WIN - 1);
+        if (count_nib(X.s, sid, nib_range(X.rp + 1, wtop)) != wtop - X.rp) return false;
+        if (X.rt >= WIN && X.xo != sid) return false;
+        const bool split = s.deep & (X.br != P.br);
+        if (s.deep & !split) return false;  // (resolve() ends a one-branch deep episode within the step)
+        int d = 0;  // lowest window height of the fork
+        uint32_t below = 0;  // fork blocks below the window (per branch)
+        if (!split) {
+            d = first_diff(X.s, P.s, P.rt);
+        } else {
+            const int pa = P.br ? C_B : C_A, xa = X.br ? C_B : C_A;
+            for (int j = 0; j < M; ++j) {
+                const uint32_t cp = env.get(pa, (uint32_t)j), cx = env.get(xa, (uint32_t)j);
+                if (((uint32_t)j == sid && cp) || ((uint32_t)j != sid && cx)) return false;
+                below += cp;
+            }
+        }
+        const int n = P.rt - d + 1;  // fork heights inside the window
+        if (count_nib(P.s, sid, nib_range(d, P.rt)) != 0 || count_nib(X.s, sid, nib_range(d, P.rt)) != n) return false;
+        const uint32_t hh = below + (uint32_t)n;
+        if (hh) {
+            if (hh >= 0xFFFFu) return false;
+            const uint32_t pas = s.hm;  // every honest miner is passive
+            const uint32_t pi = pas ? (uint32_t)__builtin_ctz(pas) : 99u;
+            if (!((P.pa < X.pa) | ((P.pa == X.pa) & (pi < sid)))) return false;
+        }
+        // convert: the common part joins the settled counters, the fork's blocks and the withheld ones are
+        // counted provisionally, the honest branch's composition goes to pend[]
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) pend[i] = 0;
+        if (split) {
+            const int pa = P.br ? C_B : C_A;
+            for (int j = 0; j < M; ++j) {
+                const uint32_t cp = env.get(pa, (uint32_t)j);
+                pend[j >> 1] += cp << (16 * (j & 1));
+                env.add(C_F, (uint32_t)j, cp);
+                env.set(C_A, (uint32_t)j, 0u);
+                env.set(C_B, (uint32_t)j, 0u);
+            }
+        }
+        for (int j = 0; j <= P.rt; ++j) {
+            const uint32_t o = (uint32_t)(P.s >> (4 * j)) & 15u;
+            env.add(C_F, o, 1u);
+            if (j >= d) pend[o >> 1] += 1u << (16 * (o & 1u));
+        }
+        const uint32_t wn = (uint32_t)s.w[0];
+        if (wn + hh) env.add(C_F, sid, wn + hh);
+        F = s.wb + (uint32_t)P.rt - hh;
+        h = hh;
+        w = wn;
+        sst = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) st[j] = 0;
+        T = s.nbt_;
+        k = s.kn_;
+        return true;
+    }
+};
+
+}  // namespace msim

@@ -6,6 +6,7 @@
 
 #include "../../miningsimulation_amd/csrc/msim_dispatch.h"
 #include "../../miningsimulation_amd/csrc/msim_sel.h"
+#include "../../miningsimulation_amd/csrc/msim_selm.h"
 
 using namespace msim;
 
@@ -36,7 +37,26 @@ struct HostSrc {
     const uint64_t *cum;  // cumulative weights
     int m;
     uint64_t W, mult;
+    uint32_t hI = 0, hk = 0;  // drawn by peek(), not yet consumed
+    bool held = false;
+    bool peek(uint32_t &I, uint32_t &k)
+    {
+        if (!held) {
+            draw(hI, hk);
+            held = true;
+        }
+        I = hI;
+        k = hk;
+        return true;
+    }
+    void pop() { held = false; }
     bool next(uint32_t &I, uint32_t &k)
+    {
+        peek(I, k);
+        pop();
+        return true;
+    }
+    void draw(uint32_t &I, uint32_t &k)
     {
         I = (uint32_t)next_interval(ri);
         const uint64_t u = rng_next(rp);
@@ -44,7 +64,6 @@ struct HostSrc {
         uint32_t f = 0;
         while ((int)f < m && cum[f] <= q) ++f;
         k = f;  // == m: fell through (simulation.h:220)
-        return true;
     }
 };
 
@@ -61,11 +80,80 @@ void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D,
     s.run(env, src, D, o);
 }
 
+// The device E1 schedule for one lane (msim_sel_kernels.hip): the settled-state form (msim_selm.h) while
+// it applies, the entity engine from a find that needs it until the network is quiet again.
+struct MixStats {
+    uint64_t macro_steps, exact_steps, entries;
+};
+MixStats g_mix;
+
+template <int M, int NS, int NA, int NG, int NQ, int NC>
+void run_mixed(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
+{
+    HostEnv env;
+    env.props = prop;
+    memset(env.c, 0, sizeof(env.c));
+    memset(env.cs, 0, sizeof(env.cs));
+    env.fold_every = g_fold_every;
+    Sel<M, NS, NA, NG, NQ, NC> s;
+    SelMacro<M> mc;
+    s.init((uint32_t)M, sids);
+    const uint32_t sid = sids[0];
+    if (!mc.begin(src)) {
+        o.err = SERR_DRAWS;
+        return;
+    }
+    bool macro = true;
+    if (mc.T >= D) {
+        mc.finish(env, sid, o);
+        return;
+    }
+    for (;;) {
+        if (macro) {
+            ++g_mix.macro_steps;
+            const int r = mc.step(env, src, D, sid, prop[sid]);
+            if (r == 2) {
+                mc.finish(env, sid, o);
+                return;
+            }
+            if (r == 1) {
+                ++g_mix.entries;
+                mc.to_exact(env, s, (uint32_t)M, sids);
+                macro = false;
+            }
+        } else {
+            ++g_mix.exact_steps;
+            if (!s.step(env, src, D)) {
+                s.finish(env, D, o);
+                return;
+            }
+            if (mc.take_back(env, s, sid)) {
+                if (mc.T >= D) {
+                    mc.finish(env, sid, o);
+                    return;
+                }
+                macro = true;
+            }
+        }
+    }
+}
+
 template <int M, int NS>
 void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
 {
     // 0: the device E1 capacities (msim_sel_launch.h), 3: a wider register class, 1: retry capacities,
     // 2: one hot slot of everything (the cold paths run constantly), 4: no cold slots (error paths)
+    if (caps >= 10 && NS == 1) {  // the mixed schedule (settled form + engine), engine capacities caps - 10
+        bool ok = true;
+        for (int k = 0; k < M; ++k) ok = ok && prop[k] >= 1;
+        if (ok) {
+            if (caps == 10) run_mixed<M, NS, 2, 4, 2, 4>(prop, sids, src, D, o);
+            else run_mixed<M, NS, 1, 4, 1, 6>(prop, sids, src, D, o);
+            return;
+        }
+        caps -= 10;
+    }
+    if (caps >= 10) caps -= 10;
     if (caps == 0) run_one<M, NS, 2, 4, 2, 4>(prop, sids, src, D, o);
     else if (caps == 1) run_one<M, NS, 4, 16, 4, 6>(prop, sids, src, D, o);
     else if (caps == 2) run_one<M, NS, 1, 4, 1, 6>(prop, sids, src, D, o);
@@ -77,6 +165,15 @@ void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src,
 
 // Early folds in every later sel_run: 0 = only when due, n = also at every n-th event.
 extern "C" void sel_set_fold_every(uint32_t n) { g_fold_every = n; }
+
+// Counters of the mixed schedule since the last call (macro steps, engine steps, hand-overs).
+extern "C" void sel_mix_stats(uint64_t *out)
+{
+    out[0] = g_mix.macro_steps;
+    out[1] = g_mix.exact_steps;
+    out[2] = g_mix.entries;
+    g_mix = MixStats{0, 0, 0};
+}
 
 // weights[m] summing to W, prop[m], selfish[m]; caps: see run_caps.
 extern "C" int sel_run(const uint64_t *weights, const int64_t *prop, const uint8_t *selfish, int m, uint64_t W,

@@ -227,3 +227,69 @@ def test_early_folds(sel, oracle, every):
                    caps=1)
     finally:
         sel.fold_every(0)
+
+
+# ---------------------------------------------------------------- the settled-state form (msim_selm.h)
+# caps 10 / 11: the device E1 schedule for one lane — the settled form while it applies, the entity engine
+# (device capacities / one hot slot of everything) from a find that needs it until the run is settled again.
+
+def _mix_stats(native_tests):
+    lib = ctypes.CDLL(native_tests["sel_host"])
+    out = (ctypes.c_uint64 * 3)()
+    lib.sel_mix_stats(out)
+    return list(out)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_mixed_random_networks(sel, oracle, seed):
+    """Random networks with one selfish miner at any index, uniform and heterogeneous delays (>= 1 ms, where
+    the settled form applies), durations from 0 ms to a month: bit-exact with the oracle."""
+    rng = random.Random(8080 + seed)
+    for _ in range(30):
+        m = rng.randint(1, 12)
+        percs = _rand_percs(m, rng)
+        s = rng.randrange(m)
+        selfish = [k == s for k in range(m)]
+        if rng.random() < 0.6:
+            props = [rng.choice([1, 2, 100, 1000, 10_000, 30_000, 120_000])] * m
+        else:
+            props = [rng.choice([1, 5, 1000, 20_000, 60_000]) for _ in range(m)]
+        duration = rng.choice([0, 1, 1000, 600_000, 86_400_000, D // 12])
+        _check(sel, oracle, percs, props, selfish, duration, rng.randrange(2**32), rng.randrange(2**32),
+               caps=rng.choice([10, 11]))
+
+
+@pytest.mark.parametrize("h,prop", [(40, 1000), (49, 30_000), (49, 1000), (10, 100), (25, 5000), (45, 20_000)])
+def test_mixed_full_year(sel, oracle, native_tests, h, prop):
+    """configs[2] and corners of the configs[3] grid, a full year each: bit-exact, and the settled form
+    carries most finds (the engine runs only around finds whose consequences overlap the next find)."""
+    percs = [h, 59 - h, 12, 11, 8, 5, 3, 1, 1]
+    _mix_stats(native_tests)
+    for r in range(2):
+        _check(sel, oracle, percs, [prop] * 9, [True] + [False] * 8, D, 1000 + 2 * r, 1001 + 2 * r, caps=10)
+    macro, exact, entries = _mix_stats(native_tests)
+    assert macro > 2 * exact and entries > 0
+
+
+def test_mixed_edge_cases(sel, oracle):
+    """Zero-length runs, a lone selfish miner, 0 % miners, the selfish miner last, 1 ms delays (the tightest
+    settle condition), and a selfish majority (tie forks of hundreds of blocks)."""
+    _check(sel, oracle, [100], [500], [True], 10**9, 5, 6, caps=10)
+    _check(sel, oracle, [30, 0, 70], [1000, 1000, 1000], [False, True, False], 10**9, 9, 10, caps=10)
+    _check(sel, oracle, [10, 20, 30, 40], [1000] * 4, [False, False, False, True], 10**9, 11, 12, caps=10)
+    _check(sel, oracle, [40, 60], [1, 1], [True, False], 10**9, 13, 14, caps=10)
+    _check(sel, oracle, [40, 60], [1, 2], [False, True], D, 13, 14, caps=11)
+    _check(sel, oracle, [70, 30], [1000, 1000], [True, False], D // 4, 15, 16, caps=10)
+    for dur in (0, 1, 2, 599_999, 600_000):
+        _check(sel, oracle, [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, dur, 1, 2, caps=10)
+
+
+def test_mixed_equals_engine_alone(sel):
+    """The schedule only changes which form advances a run: the engine alone (caps 0) and the mixed
+    schedule give the same counters on 200 runs of configs[2]."""
+    percs, props, selfish = [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8
+    for r in range(200):
+        a = sel(percs, props, selfish, D // 52, 5000 + 2 * r, 5001 + 2 * r, 0)
+        b = sel(percs, props, selfish, D // 52, 5000 + 2 * r, 5001 + 2 * r, 10)
+        assert a[0] == 0 and b[0] == 0
+        assert np.array_equal(a[1], b[1]) and a[2] == b[2]
