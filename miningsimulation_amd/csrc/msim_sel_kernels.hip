@@ -183,19 +183,22 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 }
 
 // The mixed schedule of a network with one selfish miner (msim_selm.h): every lane runs the settled-state
-// form until one of its finds needs the entity engine, then waits; the wave switches to engine steps when
-// SEL_XTH lanes wait (or no lane is left in the settled form) and back when fewer than SEL_XLO lanes are in
-// the engine, so both phases run with most lanes active. Lane modes: 0 settled form, 1 waiting for the
-// engine, 2 in the engine, 3 done. The schedule only decides the order in which lanes advance: each lane's
-// result is that of its own sequence of transitions (tests/native/sel_host.cpp runs one lane alone).
+// form until one of its finds needs the entity engine, then waits; when SEL_XTH lanes wait (or no lane is
+// left in the settled form) the wave runs an engine phase: the waiting lanes enter the engine, which steps
+// every one of them until it hands its run back (episodes are short: 5-6 events on average, 13 at the
+// 99th percentile over the configs[3] grid) or finishes it. The engine's state exists only inside a phase,
+// so its registers and the settled form's are never live at the same time. Lane modes: 0 settled form,
+// 1 waiting for the engine, 2 in the engine, 3 done. The schedule only decides the order in which lanes
+// advance: each lane's result is that of its own sequence of transitions (tests/native/sel_host.cpp runs
+// one lane alone). A network the settled form does not cover (P->macro == 0) runs one engine phase.
 #ifndef SEL_XTH
 #define SEL_XTH 16
 #endif
-#ifndef SEL_XLO
-#define SEL_XLO 4
+#ifndef SEL_MC_LDS
+#define SEL_MC_LDS 1  // the settled-form state waits in LDS during engine phases
 #endif
-template <int M, class Env, class Src, class S>
-__device__ __forceinline__ void sel_mixed(Env &env, Src &src, S &s, const SelParams *P, int64_t D, SelOut &o)
+template <int M, class SelT, class Env, class Src>
+__device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P, int64_t D, SelOut &o, uint32_t *mcs)
 {
     SelMacro<M> mc;
     // A lane that finishes parks its counters in its own LDS counter rows (C_F, C_S) so that no result
@@ -215,8 +218,7 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, S &s, const SelPar
     const bool mac = P->macro != 0u;  // wave-uniform (one point per workgroup)
     int mode = 0;
     if (!mac) {  // the entity engine for every find
-        s.begin(src);
-        mode = 2;
+        mode = 1;
     } else if (!mc.begin(src)) {
         err = SERR_DRAWS;
         mode = 3;
@@ -228,13 +230,22 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, S &s, const SelPar
     }
     for (;;) {
         const uint64_t bm = __builtin_amdgcn_ballot_w64(mode == 0);
-        const uint64_t be = __builtin_amdgcn_ballot_w64(mode == 1 || mode == 2);
+        const uint64_t be = __builtin_amdgcn_ballot_w64(mode == 1);
         if ((bm | be) == 0ull) break;
         if (be != 0ull && (__builtin_popcountll(be) >= SEL_XTH || bm == 0ull)) {
+            SelT s;
             if (mode == 1) {
-                mc.to_exact(env, s, P->m, P->sids);
+                if (mac) {
+                    mc.to_exact(env, s, P->m, P->sids);
+                } else {
+                    s.init(P->m, P->sids);
+                    s.begin(src);
+                }
                 mode = 2;
             }
+#if SEL_MC_LDS
+            mc.save(mcs, TPB);  // saved and reloaded for every lane: no settled-form register is live here
+#endif
             for (;;) {
                 if (mode == 2) {
                     src.prefetch();
@@ -245,20 +256,30 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, S &s, const SelPar
                         s.finish(env, D, r);
                         park(r);
                         mode = 3;
-                    } else if (mac && mc.take_back(env, s, sid)) {
-                        if (mc.T >= D) {
-                            SelOut r;
-                            mc.finish(env, sid, r);
-                            park(r);
-                            mode = 3;
-                        } else {
-                            mode = 0;
+                    } else if (mac) {
+                        SelMacro<M> tb;
+                        if (tb.take_back(env, s, sid)) {
+                            if (tb.T >= D) {
+                                SelOut r;
+                                tb.finish(env, sid, r);
+                                park(r);
+                                mode = 3;
+                            } else {
+#if SEL_MC_LDS
+                                tb.save(mcs, TPB);
+#else
+                                mc = tb;
+#endif
+                                mode = 0;
+                            }
                         }
                     }
                 }
-                const uint64_t b2 = __builtin_amdgcn_ballot_w64(mode == 2);
-                if (__builtin_popcountll(b2) < SEL_XLO && (b2 == 0ull || __builtin_amdgcn_ballot_w64(mode == 0) != 0ull)) break;
+                if (__builtin_amdgcn_ballot_w64(mode == 2) == 0ull) break;
             }
+#if SEL_MC_LDS
+            mc.load(mcs, TPB);
+#endif
         } else {
             for (;;) {
                 if (mode == 0) {
@@ -274,7 +295,7 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, S &s, const SelPar
                     }
                 }
                 if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
-                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 1 || mode == 2)) >= SEL_XTH)
+                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 1)) >= SEL_XTH)
                     break;
             }
         }
@@ -293,6 +314,7 @@ template <int M, int NS, int NA, int NG, int NQ, int NC>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_sel_kernel(const SelArgs a)
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
+    __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
     __shared__ int64_t s_prop[MAXM];
     const uint32_t tid = threadIdx.x;
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
@@ -316,16 +338,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         src.row = (size_t)a.nr * (SEL_TILE / 4);
         src.nb = a.nb;
         src.init(P->ccum);
-        Sel<M, NS, NA, NG, NQ, NC> s;
-        s.init(P->m, P->sids);
         SelOut o;
         const int64_t D = P->duration_ms;
         if (a.force_retry) {
             o.err = SERR_CAP;
         } else {
             if constexpr (NS == 1) {
-                sel_mixed<M>(env, src, s, P, D, o);
+                sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid]);
             } else {
+                Sel<M, NS, NA, NG, NQ, NC> s;
+                s.init(P->m, P->sids);
                 s.begin(src);
                 for (;;) {
                     src.prefetch();
@@ -401,7 +423,12 @@ template <int M, int NS>
 static hipError_t launch_sel_ns(const SelArgs &a, hipStream_t s)
 {
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
-    hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+    // one selfish miner: the mixed schedule, whose engine episodes are local (one hot slot of each kind
+    // flags no run of the configs[3] grid, tests/test_sel_host.py)
+    if constexpr (NS == 1)
+        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 2, 1, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+    else
+        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
     return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@
 // quiet again (a common published chain, only withheld blocks on top) and hands the run back.
 //
 // Counters: found[k] is counted provisionally at every find (the LDS C_F array); blocks that later leave
-// the best chain (stale honest branches: st[], stale selfish tie blocks: sst; the honest branch's
+// the best chain (stale honest branches: stp[], stale selfish tie blocks: sst; the honest branch's
 // composition is kept as 16-bit counts per miner in pend[]) are subtracted when they are flushed.
 #pragma once
 #include "msim_sel.h"
@@ -41,8 +41,43 @@ struct SelMacro {
     uint32_t k;            // its finder
     uint32_t F, h, w;      // settled state (see above)
     uint32_t pend[NPW];    // honest branch: blocks per honest miner, 16 bits each
-    uint32_t st[M];        // honest stale blocks not yet flushed to C_S
+    uint32_t stp[NPW];     // honest stale blocks not yet flushed to C_S, same packing
     uint32_t sst;          // selfish stale blocks not yet flushed
+    uint32_t Ff;           // F at the last flush (stale added since <= F - Ff keeps stp's fields < 2^16)
+
+    // The state as NW words at p[0], p[stride], ... (a lane's LDS column while the wave runs engine steps).
+    static constexpr int NW = 8 + 2 * NPW;
+    MSIM_HD void save(uint32_t *p, int stride) const
+    {
+        p[0] = (uint32_t)T;
+        p[stride] = (uint32_t)((uint64_t)T >> 32);
+        p[2 * stride] = k;
+        p[3 * stride] = F;
+        p[4 * stride] = h;
+        p[5 * stride] = w;
+        p[6 * stride] = sst;
+        p[7 * stride] = Ff;
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) {
+            p[(8 + i) * stride] = pend[i];
+            p[(8 + NPW + i) * stride] = stp[i];
+        }
+    }
+    MSIM_HD void load(const uint32_t *p, int stride)
+    {
+        T = (int64_t)(((uint64_t)p[stride] << 32) | p[0]);
+        k = p[2 * stride];
+        F = p[3 * stride];
+        h = p[4 * stride];
+        w = p[5 * stride];
+        sst = p[6 * stride];
+        Ff = p[7 * stride];
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) {
+            pend[i] = p[(8 + i) * stride];
+            stp[i] = p[(8 + NPW + i) * stride];
+        }
+    }
 
     MSIM_HD uint32_t pend_of(int j) const { return (pend[j >> 1] >> (16 * (j & 1))) & 0xFFFFu; }
 
@@ -54,10 +89,9 @@ struct SelMacro {
         h = 0;
         w = 0;
         sst = 0;
+        Ff = 0;
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) pend[i] = 0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) st[j] = 0;
+        for (int i = 0; i < NPW; ++i) pend[i] = stp[i] = 0;
         uint32_t I = 0;
         if (!src.peek(I, k)) return false;
         src.pop();
@@ -85,7 +119,7 @@ struct SelMacro {
 #pragma unroll
         for (int i = 0; i < NPW; ++i) pend[i] += (k >> 1) == (uint32_t)i ? inc : 0u;
 #pragma unroll
-        for (int j = 0; j < M; ++j) st[j] += swin ? pend_of(j) : 0u;
+        for (int i = 0; i < NPW; ++i) stp[i] += swin ? pend[i] : 0u;
         sst += res ? h : 0u;
         F += res ? h + 1u : (swin ? h + 2u : 0u);
         h = (res | swin) ? 0u : h + (tie ? 1u : 0u);
@@ -93,6 +127,7 @@ struct SelMacro {
 #pragma unroll
         for (int i = 0; i < NPW; ++i) pend[i] = (res | swin) ? 0u : pend[i];
         env.add(C_F, k, 1u);
+        if (F - Ff >= 0xFF00u) flush_stale(env, sid);
         src.pop();
         T += (int64_t)I;
         k = kn;
@@ -103,12 +138,16 @@ struct SelMacro {
     MSIM_HD void flush_stale(Env &env, uint32_t sid)
     {
 #pragma unroll
-        for (int j = 0; j < M; ++j)
-            if (st[j]) {
-                env.add(C_S, (uint32_t)j, st[j]);
-                env.add(C_F, (uint32_t)j, 0u - st[j]);
-                st[j] = 0;
+        for (int j = 0; j < M; ++j) {
+            const uint32_t v = (stp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            if (v) {
+                env.add(C_S, (uint32_t)j, v);
+                env.add(C_F, (uint32_t)j, 0u - v);
             }
+        }
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) stp[i] = 0;
+        Ff = F;
         if (sst) {
             env.add(C_S, sid, sst);
             env.add(C_F, sid, 0u - sst);
@@ -236,8 +275,9 @@ struct SelMacro {
         h = hh;
         w = wn;
         sst = 0;
+        Ff = F;
 #pragma unroll
-        for (int j = 0; j < M; ++j) st[j] = 0;
+        for (int i = 0; i < NPW; ++i) stp[i] = 0;
         T = s.nbt_;
         k = s.kn_;
         return true;

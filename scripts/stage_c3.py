@@ -10,4 +10,4 @@ sums = torch.zeros((9, 6), dtype=torch.int64, device="cuda"); st = torch.zeros(2
 sim.launch(n, 0, 1000, sums, ws, st); torch.cuda.synchronize()
 m.timing_enable(True)
 sim.launch(n, n, 1000, sums, ws, st); torch.cuda.synchronize()
-print("c3", n, m.timing_read(), "status", st.tolist(), flush=True)
+print("c3", n, m.timing_read(), "status", st.tolist(), "found/stale", sums[:, :2].sum(1).tolist() if False else sums[:, :2].tolist(), flush=True)
