@@ -4,8 +4,10 @@
 // draw j*SEG (msim_jump.h), then the lane produces SEG blocks exactly as the reference's sequential
 // loop would draw them (simulation.h:205-221): interval I_i (ms), finder k_i, and the "fast" bit
 // I_{i+1} > prop_{k_i} (honest finders only). A wave = 64 consecutive runs at one segment, so the
-// jump matrix columns are wave-uniform scalar loads and every 4-block store is one coalesced 1 KiB
-// wave store. Roofline: VALU issue (FP64 log + 64-bit integer RNG); the word stream is 4 B/block.
+// jump matrix columns are wave-uniform scalar loads. Nothing is stored per block: a non-fast block is
+// listed with both RNG states (K2 redraws its episode), and each group of the band where a run can end
+// keeps its first word and RNG states (K3 redraws the last group). Roofline: VALU issue (FP64 log +
+// 64-bit integer RNG).
 #include <hip/hip_runtime.h>
 
 #include "msim_jump.h"
@@ -45,16 +47,16 @@ __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rn
     b.s1 = (uint64_t)ob2 | ((uint64_t)ob3 << 32);
 }
 
-// Side effects of one K1 lane (msim_pipeline.h draw_segment): LDS per-owner counters, coalesced
-// word stores, wave-aggregated appends to the dense episode list.
+// Side effects of one K1 lane (msim_pipeline.h draw_segment): LDS per-owner counters, wave-aggregated
+// appends to the dense episode list, the band's group records.
 struct DevCtx {
     const DrawArgs &a;
     uint32_t (*cnt)[256];
     uint32_t tid, lane, r, seg, jb, nsl;
     bool active;
-    uint4 *wout;
     __device__ void count(uint32_t k) { atomicAdd(&cnt[k >> 1][tid], 1u << (16u * (k & 1u))); }
-    __device__ void slow(bool is_slow, uint32_t block, uint64_t offset)
+    __device__ void slow(bool is_slow, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri,
+                         const Rng &rp)
     {
         const bool want = is_slow && active;
         const uint64_t mask = __ballot(want);
@@ -71,18 +73,25 @@ struct DevCtx {
             e.run = r;
             e.block = block;
             e.offset = offset;
+            e.w0 = w0;
+            e.w1 = w1;
+            e.pad[0] = e.pad[1] = 0;
+            e.ri = ri;
+            e.rp = rp;
             a.list[idx] = e;
         }
         if (nsl < a.cap) a.slots[((size_t)seg * a.cap + nsl) * a.nr + r] = idx;
         ++nsl;
     }
-    __device__ void store4(uint32_t q4, uint32_t x, uint32_t y, uint32_t z, uint32_t w)
-    {
-        wout[(size_t)q4 * a.nr] = make_uint4(x, y, z, w);
-    }
-    __device__ void group_start(uint32_t g)
+    __device__ void group_start(uint32_t g, uint32_t w0, const Rng &ri, const Rng &rp)
     {
         const size_t gi = (size_t)jb * a.gps + g;
+        GroupRec gr;
+        gr.ri = ri;
+        gr.rp = rp;
+        gr.w0 = w0;
+        gr.pad = 0;
+        a.grec[gi * a.nr + r] = gr;
 #pragma unroll
         for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = cnt[w][tid];
     }
@@ -116,8 +125,7 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
 
     const uint32_t b0 = seg * a.seg;
-    DevCtx cx{a, s_cnt, tid, tid & 63u, r, seg, seg - a.band_lo, 0u, r < a.n,
-              reinterpret_cast<uint4 *>(a.words) + (size_t)(b0 >> 2) * a.nr + r};
+    DevCtx cx{a, s_cnt, tid, tid & 63u, r, seg, seg - a.band_lo, 0u, r < a.n};
     const uint64_t tsum = draw_segment(cx, ri, rp, s_log, s_pick, b0, a.seg, seg >= a.band_lo);
     a.segsum[(size_t)seg * a.nr + r] = tsum;
 #pragma unroll

@@ -150,6 +150,9 @@ __global__ __launch_bounds__(TPB, 2) void msim_sweep_kernel(const SimParams *__r
 }
 
 // ------------------------------------------------------------------ event-skipping pipeline (K2, K3)
+// K2 / K3 redraw blocks (msim_pipeline.h draw_word); the exact interval is out of line, as in K1.
+__device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
+
 // K2: one lane per listed non-fast block (msim_pipeline.h episode_entry).
 template <int M>
 __global__ __launch_bounds__(TPB) void msim_episode_kernel(const SimParams p, const PipeArgs a)
@@ -237,13 +240,14 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     pa.band_lo = L.band_lo;
     pa.lcap = L.lcap;
     pa.rec_words = L.rec_words;
-    pa.words = (const uint32_t *)(ws + L.words_off);
+    pa.tab = a.tab;
     pa.segsum = (const uint64_t *)(ws + L.segsum_off);
     pa.segcnt = (const uint32_t *)(ws + L.segcnt_off);
     pa.nslow = (const uint32_t *)(ws + L.nslow_off);
     pa.slots = (const uint32_t *)(ws + L.slots_off);
     pa.gsum = (const uint32_t *)(ws + L.gsum_off);
     pa.gcum = (const uint32_t *)(ws + L.gcum_off);
+    pa.grec = (const GroupRec *)(ws + L.grec_off);
     pa.list = (const EpEntry *)(ws + L.list_off);
     pa.list_count = (const uint32_t *)(ws + L.count_off);
     pa.recs = (uint32_t *)(ws + L.recs_off);
@@ -257,13 +261,13 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.cap = L.cap;
     da.band_lo = L.band_lo;
     da.lcap = L.lcap;
-    da.words = (uint32_t *)(ws + L.words_off);
     da.segsum = (uint64_t *)(ws + L.segsum_off);
     da.segcnt = (uint32_t *)(ws + L.segcnt_off);
     da.nslow = (uint32_t *)(ws + L.nslow_off);
     da.slots = (uint32_t *)(ws + L.slots_off);
     da.gsum = (uint32_t *)(ws + L.gsum_off);
     da.gcum = (uint32_t *)(ws + L.gcum_off);
+    da.grec = (GroupRec *)(ws + L.grec_off);
     da.list = (EpEntry *)(ws + L.list_off);
     da.list_count = (uint32_t *)(ws + L.count_off);
     uint32_t ep_grid = (L.lcap + TPB - 1) / TPB;

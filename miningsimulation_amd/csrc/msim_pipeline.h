@@ -7,9 +7,11 @@
 // a pure function of the draws from its first block on (translation-invariant in time apart from the
 // end of the run). So one run is computed as
 //
-//   K1 msim_draws_kernel    (run, segment) workers, jump-ahead to draw j*SEG, produce every block's
-//                           word (interval, fast bit, finder), per-segment time and per-owner counts,
-//                           and append every non-fast block to a dense episode list;
+//   K1 msim_draws_kernel    (run, segment) workers, jump-ahead to draw j*SEG, draw every block
+//                           (interval, finder, fast bit), keep per-segment time and per-owner counts,
+//                           and append every non-fast block to a dense episode list together with both
+//                           RNG states there; nothing is stored per block (the band where a run can end
+//                           keeps per-group sums, counts and the RNG states at each group start);
 //   K2 msim_episode_kernel  one lane per listed block: the full state machine (msim_model.h) from a
 //                           quiet state at that block, until quiet again or the end of the run;
 //   K3 msim_combine_kernel  one lane per run: locate the end of the run (first T_i >= D), chain the
@@ -36,6 +38,16 @@ struct EpEntry {
     uint32_t run;     // slice-local run
     uint32_t block;   // block index within the run
     uint64_t offset;  // T_block - (start time of its segment), ms
+    uint32_t w0, w1;  // (interval << 5 | finder) of the block and of the next one
+    uint32_t pad[2];
+    Rng ri, rp;       // both streams, positioned at the block after w1
+};
+
+// A group of the band (where a run can end): the first block's word and both streams after it.
+struct GroupRec {
+    Rng ri, rp;
+    uint32_t w0;
+    uint32_t pad;
 };
 
 struct PipeLayout {
@@ -49,7 +61,7 @@ struct PipeLayout {
     uint32_t nband;
     uint32_t lcap;     // episode list capacity
     uint32_t rec_words;
-    size_t words_off, segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gcum_off, list_off, recs_off,
+    size_t segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gcum_off, grec_off, list_off, recs_off,
         count_off, total;
 };
 
@@ -66,52 +78,33 @@ struct DrawArgs {
     uint32_t n;           // valid runs in the slice
     uint32_t seed_base;
     uint32_t nr, seg, gps, nseg, cap, band_lo, lcap;
-    uint32_t *words;      // [nb/4][nr][4]
     uint64_t *segsum;     // [nseg][nr]
     uint32_t *segcnt;     // [nseg][8][nr]
     uint32_t *nslow;      // [nseg][nr]
     uint32_t *slots;      // [nseg][cap][nr]
     uint32_t *gsum;       // [nband][gps][nr]
     uint32_t *gcum;       // [nband][gps][8][nr]
+    GroupRec *grec;       // [nband][gps][nr]
     EpEntry *list;        // [lcap]
     uint32_t *list_count;
 };
 
 struct PipeArgs {  // K2 / K3
     uint32_t nr, seg, gps, nseg, nb, cap, band_lo, lcap, rec_words;
-    const uint32_t *words;
+    PipeTables tab;       // K2 / K3 redraw blocks from stored RNG states
     const uint64_t *segsum;
     const uint32_t *segcnt;
     const uint32_t *nslow;
     const uint32_t *slots;
     const uint32_t *gsum;
     const uint32_t *gcum;
+    const GroupRec *grec;
     const EpEntry *list;
     const uint32_t *list_count;
     uint32_t *recs;       // [lcap][rec_words]: end, flags, F[M], S[M]
 };
 
 enum : uint32_t { REC_ENDED = 1u, REC_ERR = 2u, REC_SKIP = 4u };
-
-MSIM_HD size_t word_index(uint32_t nr, uint32_t run, uint32_t block)
-{
-    return ((size_t)(block >> 2) * nr + run) * 4 + (block & 3u);
-}
-
-// Episode draw source: the words of one run, from a given block on.
-struct WordSrc {
-    const uint32_t *words;
-    uint32_t nr, nb, run, index;
-    uint32_t cur;
-    MSIM_HD uint32_t word() const { return cur; }
-    MSIM_HD bool advance()
-    {
-        if (index + 1 >= nb) return false;
-        ++index;
-        cur = words[word_index(nr, run, index)];
-        return true;
-    }
-};
 
 // ---------------------------------------------------------------- sizing (host)
 // Every capacity has a >= 8-sigma margin; a run that exceeds one anyway is recomputed by the retry
@@ -131,8 +124,9 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     // slice size first (memory), with an upper estimate of the per-run bytes
     L.rec_words = 2 + 2 * m;
     const double nb_est = need + 2.0 * MIN_SEG;
-    const double per_run = nb_est * 4.0 + 64.0 * (8.0 + CNT_WORDS * 4 + 4) + 4.0 * (rho * nb_est * 2 + 64.0 * 16) +
-                           2.0 * nb_est / GROUP * (4.0 + CNT_WORDS * 4) + rho * nb_est * (sizeof(EpEntry) + 4.0 * L.rec_words);
+    const double per_run = 64.0 * (8.0 + CNT_WORDS * 4 + 4) + 4.0 * (rho * nb_est * 2 + 64.0 * 16) +
+                           2.0 * nb_est / GROUP * (4.0 + CNT_WORDS * 4 + sizeof(GroupRec)) +
+                           rho * nb_est * (sizeof(EpEntry) + 4.0 * L.rec_words);
     uint64_t cap_runs = (uint64_t)(budget / per_run) / 256 * 256;
     if (cap_runs < 256) cap_runs = 256;
     L.nr = (uint32_t)(want < cap_runs ? want : cap_runs);
@@ -165,8 +159,6 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     const double ent = (double)L.nr * rho * L.nb;
     L.lcap = (uint32_t)ceil(ent + 8.0 * sqrt(ent) + 1024.0);
     size_t o = 0;
-    L.words_off = o;
-    o = al(o + (size_t)L.nb * L.nr * 4);
     L.segsum_off = o;
     o = al(o + (size_t)L.nseg * L.nr * 8);
     L.segcnt_off = o;
@@ -179,6 +171,8 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     o = al(o + (size_t)L.nband * L.gps * L.nr * 4);
     L.gcum_off = o;
     o = al(o + (size_t)L.nband * L.gps * CNT_WORDS * L.nr * 4);
+    L.grec_off = o;
+    o = al(o + (size_t)L.nband * L.gps * L.nr * sizeof(GroupRec));
     L.list_off = o;
     o = al(o + (size_t)L.lcap * sizeof(EpEntry));
     L.recs_off = o;
@@ -206,13 +200,43 @@ MSIM_HD uint32_t draw_interval(Rng &ri, const LogEntry *__restrict__ lt)
 #endif
 }
 
+// Both draws of one block as a word: interval << 5 | finder (pick_info's low nibble).
+MSIM_HD uint32_t draw_word(Rng &ri, Rng &rp, const LogEntry *__restrict__ lt, const PickEntry *__restrict__ pt)
+{
+    const uint32_t I = draw_interval(ri, lt);
+    return (I << 5) | (pick_info(rng_next(rp), pt) & 15u);
+}
+
+// Episode draw source (K2): the stored words of its first two blocks, then the streams redrawn.
+struct EpSrc {
+    const LogEntry *lt;
+    const PickEntry *pt;
+    Rng ri, rp;
+    uint32_t nb, index, cur, nxt;
+    bool have_nxt;
+    MSIM_HD uint32_t word() const { return cur; }
+    MSIM_HD bool advance()
+    {
+        if (index + 1 >= nb) return false;  // past the pre-generated budget: the run is retried
+        ++index;
+        if (have_nxt) {
+            cur = nxt;
+            have_nxt = false;
+        } else {
+            cur = draw_word(ri, rp, lt, pt);
+        }
+        return true;
+    }
+};
+
 // One (run, segment) worker: SEG blocks from the jumped RNG states. Ctx supplies the side effects:
-//   count(k)                per-owner counter of this lane (+1 for owner k)
-//   snapshot(w)             packed counter word w (u16 pairs)
-//   slow(block, offset)     a non-fast block (offset = its find time minus the segment's start)
-//   store4(q4, a, b, c, d)  words of blocks 4*q4 .. 4*q4+3 of the segment
-//   group(g, sum)           band only: sum of the group's intervals
-//   group_start(g)          band only: called before group g's first block (snapshot the counters)
+//   count(k)                          per-owner counter of this lane (+1 for owner k)
+//   slow(s, block, offset, w0, w1, ri, rp)
+//                                     a non-fast block when s (offset = its find time minus the segment's
+//                                     start; its word, the next one and both streams after them)
+//   group(g, sum)                     band only: sum of the group's intervals
+//   group_start(g, w0, ri, rp)        band only: before group g's first block (its word and the streams
+//                                     after it; snapshot the counters)
 template <class Ctx>
 MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogEntry *__restrict__ lt,
                               const PickEntry *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
@@ -222,8 +246,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogEntry *__restr
     uint64_t tsum = 0;
     uint32_t gacc = 0;
     for (uint32_t q4 = 0; q4 < seg / 4; ++q4) {
-        if (band && (q4 & 7u) == 0) cx.group_start(q4 >> 3);
-        uint32_t wv[4];
+        if (band && (q4 & 7u) == 0) cx.group_start(q4 >> 3, (Icur << 5) | (infocur & 15u), ri, rp);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t Inext = draw_interval(ri, lt);  // I_{i+1}
@@ -232,13 +255,11 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogEntry *__restr
             gacc += Icur;
             const uint32_t k = infocur & 15u;
             const bool fast = Inext > (infocur >> 4);
-            wv[q] = (Icur << 5) | (fast ? 16u : 0u) | k;
             cx.count(k);
-            cx.slow(!fast, b0 + q4 * 4 + (uint32_t)q, tsum);
+            cx.slow(!fast, b0 + q4 * 4 + (uint32_t)q, tsum, (Icur << 5) | k, (Inext << 5) | (infonext & 15u), ri, rp);
             Icur = Inext;
             infocur = infonext;
         }
-        cx.store4(q4, wv[0], wv[1], wv[2], wv[3]);
         if (band && (q4 & 7u) == 7u) {
             cx.group(q4 >> 3, gacc);
             gacc = 0;
@@ -296,27 +317,40 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     if (G == a.gps) return false;
     add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr);
     const uint32_t bg = (uint32_t)e * a.seg + G * GROUP;
-    uint32_t n_end = 0;
+    uint32_t n_end = 0, klast = 15u;
     int64_t t_last = 0;
     bool done = false;
-#pragma unroll 4
-    for (uint32_t q = 0; q < GROUP; ++q) {
-        const uint32_t wd = a.words[word_index(a.nr, r, bg + q)];
-        if (!done) {
+    {  // redraw the group from its first block's stored streams
+        const GroupRec gr = a.grec[(gb + G) * a.nr + r];
+        Rng ri = gr.ri, rp = gr.rp;
+        uint32_t wd = gr.w0;
+        for (uint32_t q = 0; q < GROUP; ++q) {
+            if (q) wd = draw_word(ri, rp, a.tab.logt, a.tab.pick);
             const int64_t Tn = T + (int64_t)(wd >> 5);
             if (Tn >= D) {
                 done = true;
                 n_end = bg + q;
                 t_last = T;
-            } else {
-                T = Tn;
-                const uint32_t k = wd & 15u;
-#pragma unroll
-                for (int kk = 0; kk < M; ++kk) F[kk] += (k == (uint32_t)kk) ? 1u : 0u;
+                break;
             }
+            T = Tn;
+            klast = wd & 15u;
+#pragma unroll
+            for (int kk = 0; kk < M; ++kk) F[kk] += (klast == (uint32_t)kk) ? 1u : 0u;
         }
     }
     if (!done) return false;
+    if (n_end == bg && n_end > 0) {  // the block before the end is the previous group's last one
+        size_t pg;
+        if (G > 0) pg = gb + G - 1;
+        else if (e > (int)a.band_lo) pg = gb - 1;
+        else return false;
+        const GroupRec gr = a.grec[pg * a.nr + r];
+        Rng ri = gr.ri, rp = gr.rp;
+        uint32_t wd = gr.w0;
+        for (uint32_t q = 1; q < GROUP; ++q) wd = draw_word(ri, rp, a.tab.logt, a.tab.pick);
+        klast = wd & 15u;
+    }
     // 3. Episodes in block order; an episode applies when its first block is reached quiet.
     uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
     bool stop = false;
@@ -350,7 +384,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     }
     // 4. The run ended quiet and its last block was a fast one: it counts only if it arrived by D.
     if (cursor != 0xFFFFFFFFu && n_end > 0 && cursor < n_end) {
-        const uint32_t k = a.words[word_index(a.nr, r, n_end - 1)] & 15u;
+        const uint32_t k = klast;
         int64_t pk = 0;
 #pragma unroll
         for (int kk = 0; kk < M; ++kk)
@@ -376,13 +410,16 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
         rec[1] = REC_SKIP;
         return;
     }
-    WordSrc src;
-    src.words = a.words;
-    src.nr = a.nr;
+    EpSrc src;
+    src.lt = a.tab.logt;
+    src.pt = a.tab.pick;
+    src.ri = e.ri;
+    src.rp = e.rp;
     src.nb = a.nb;
-    src.run = e.run;
     src.index = e.block;
-    src.cur = a.words[word_index(a.nr, e.run, e.block)];
+    src.cur = e.w0;
+    src.nxt = e.w1;
+    src.have_nxt = true;
     Sim<M, false, true, NX_WIDE, NG_WIDE> s;
     EpisodeOut<M> o;
     s.episode(p, src, T, o);

@@ -159,6 +159,8 @@ struct SelRngSrc {
         return true;
     }
     __device__ void pop() { held = false; }
+    __device__ void prefetch() {}
+    __device__ void settle() {}
 };
 
 template <int M>
@@ -194,6 +196,9 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #ifndef SEL_XTH
 #define SEL_XTH 16
 #endif
+#ifndef SEL_PROF
+#define SEL_PROF 0
+#endif
 #ifndef SEL_MC_LDS
 #define SEL_MC_LDS 1  // the settled-form state waits in LDS during engine phases
 #endif
@@ -228,10 +233,18 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
         park(r);
         mode = 3;
     }
+#if SEL_PROF  // per-wave phase timing (diagnostic builds only: scripts/build_sel_variant.sh prof -DSEL_PROF=1)
+    uint64_t pt_m = 0, pt_e = 0, pn_m = 0, pn_e = 0, pi_m = 0, pi_e = 0, pl_m = 0, pl_e = 0;
+    const uint64_t pt0 = clock64();
+#endif
     for (;;) {
         const uint64_t bm = __builtin_amdgcn_ballot_w64(mode == 0);
         const uint64_t be = __builtin_amdgcn_ballot_w64(mode == 1);
         if ((bm | be) == 0ull) break;
+#if SEL_PROF
+        const uint64_t pc0 = clock64();
+        const bool pexact = be != 0ull && (__builtin_popcountll(be) >= SEL_XTH || bm == 0ull);
+#endif
         if (be != 0ull && (__builtin_popcountll(be) >= SEL_XTH || bm == 0ull)) {
             SelT s;
             if (mode == 1) {
@@ -275,6 +288,10 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
                         }
                     }
                 }
+#if SEL_PROF
+                ++pi_e;
+                pl_e += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 2));
+#endif
                 if (__builtin_amdgcn_ballot_w64(mode == 2) == 0ull) break;
             }
 #if SEL_MC_LDS
@@ -294,12 +311,33 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
                         mode = 1;
                     }
                 }
+#if SEL_PROF
+                ++pi_m;
+                pl_m += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 0));
+#endif
                 if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
                     __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 1)) >= SEL_XTH)
                     break;
             }
         }
+#if SEL_PROF
+        const uint64_t pc1 = clock64();
+        if (pexact) {
+            pt_e += pc1 - pc0;
+            ++pn_e;
+        } else {
+            pt_m += pc1 - pc0;
+            ++pn_m;
+        }
+#endif
     }
+#if SEL_PROF
+    if (blockIdx.x < 2 && (threadIdx.x & 63u) == 0u)
+        printf("SELPROF blk %u wave %u total %llu | macro phases %llu cyc %llu iters %llu lanes %llu | engine phases %llu cyc %llu iters %llu lanes %llu\n",
+               blockIdx.x, threadIdx.x / 64u, (unsigned long long)(clock64() - pt0), (unsigned long long)pn_m,
+               (unsigned long long)pt_m, (unsigned long long)pi_m, (unsigned long long)pl_m, (unsigned long long)pn_e,
+               (unsigned long long)pt_e, (unsigned long long)pi_e, (unsigned long long)pl_e);
+#endif
 #pragma unroll
     for (int k = 0; k < M; ++k) {
         o.found[k] = env.get(C_F, (uint32_t)k);
@@ -381,6 +419,7 @@ template <int M, int NS>
 __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
+    __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
     const uint32_t tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
@@ -393,10 +432,14 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
     const uint64_t run = a.run_begin + rel;
     SelDevEnv<M> env{&s_cnt[0][tid], P->prop, P->prop[0], P->uniform_prop != 0, a.cold + idx, a.cold_lanes};
     SelRngSrc src{rng_seed(seed_interval(a.seed_base, run)), rng_seed(seed_picker(a.seed_base, run)), P};
-    Sel<M, NS, 4, 16, 4, SEL_NC> s;
-    s.init(P->m, P->sids);
     SelOut o;
-    s.run(env, src, P->duration_ms, o);
+    if constexpr (NS == 1) {  // the mixed schedule, with the engine's wide capacities
+        sel_mixed<M, Sel<M, NS, 4, 16, 4, SEL_NC>>(env, src, P, P->duration_ms, o, &s_mc[0][tid]);
+    } else {
+        Sel<M, NS, 4, 16, 4, SEL_NC> s;
+        s.init(P->m, P->sids);
+        s.run(env, src, P->duration_ms, o);
+    }
     if (o.err) {
         atomicAdd(a.counts + 1, 1u);
         return;
@@ -426,7 +469,7 @@ static hipError_t launch_sel_ns(const SelArgs &a, hipStream_t s)
     // one selfish miner: the mixed schedule, whose engine episodes are local (one hot slot of each kind
     // flags no run of the configs[3] grid, tests/test_sel_host.py)
     if constexpr (NS == 1)
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 2, 1, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
     else
         hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
     return hipGetLastError();

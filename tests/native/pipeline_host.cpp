@@ -20,27 +20,21 @@ struct HostCtx {
     PipeLayout L;
     uint32_t r, seg, jb, nsl = 0;
     uint32_t cnt[CNT_WORDS] = {0};
-    std::vector<uint32_t> *words, *slots, *gsum, *gcum;
+    std::vector<uint32_t> *slots, *gsum, *gcum;
+    std::vector<GroupRec> *grec;
     std::vector<EpEntry> *list;
     void count(uint32_t k) { cnt[k >> 1] += 1u << (16u * (k & 1u)); }
-    void slow(bool s, uint32_t block, uint64_t offset)
+    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         if (!s) return;
         const uint32_t idx = (uint32_t)list->size();
-        if (idx < L.lcap) list->push_back(EpEntry{r, block, offset});
+        if (idx < L.lcap) list->push_back(EpEntry{r, block, offset, w0, w1, {0, 0}, ri, rp});
         if (nsl < L.cap) (*slots)[((size_t)seg * L.cap + nsl) * L.nr + r] = idx;
         ++nsl;
     }
-    void store4(uint32_t q4, uint32_t x, uint32_t y, uint32_t z, uint32_t w)
+    void group_start(uint32_t g, uint32_t w0, const Rng &ri, const Rng &rp)
     {
-        const uint32_t b = seg * L.seg + q4 * 4;
-        (*words)[word_index(L.nr, r, b)] = x;
-        (*words)[word_index(L.nr, r, b + 1)] = y;
-        (*words)[word_index(L.nr, r, b + 2)] = z;
-        (*words)[word_index(L.nr, r, b + 3)] = w;
-    }
-    void group_start(uint32_t g)
-    {
+        (*grec)[((size_t)jb * L.gps + g) * L.nr + r] = GroupRec{ri, rp, w0, 0};
         for (uint32_t w = 0; w < CNT_WORDS; ++w) (*gcum)[(((size_t)jb * L.gps + g) * CNT_WORDS + w) * L.nr + r] = cnt[w];
     }
     void group(uint32_t g, uint32_t sum) { (*gsum)[((size_t)jb * L.gps + g) * L.nr + r] = sum; }
@@ -61,7 +55,8 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     build_pick_table(perc, prop, self, M, pick.data());
     build_log_table(logt.data());
     build_jump_table(L.nseg, L.seg, jump.data());
-    std::vector<uint32_t> words((size_t)L.nb * n), segcnt((size_t)L.nseg * CNT_WORDS * n), nslow((size_t)L.nseg * n),
+    std::vector<GroupRec> grec((size_t)L.nband * L.gps * n);
+    std::vector<uint32_t> segcnt((size_t)L.nseg * CNT_WORDS * n), nslow((size_t)L.nseg * n),
         slots((size_t)L.nseg * L.cap * n, 0xFFFFFFFFu), gsum((size_t)L.nband * L.gps * n),
         gcum((size_t)L.nband * L.gps * CNT_WORDS * n);
     std::vector<uint64_t> segsum((size_t)L.nseg * n);
@@ -90,7 +85,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
             cx.r = r;
             cx.seg = j;
             cx.jb = j - L.band_lo;
-            cx.words = &words;
+            cx.grec = &grec;
             cx.slots = &slots;
             cx.gsum = &gsum;
             cx.gcum = &gcum;
@@ -112,7 +107,8 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     a.band_lo = L.band_lo;
     a.lcap = L.lcap;
     a.rec_words = L.rec_words;
-    a.words = words.data();
+    a.tab = PipeTables{pick.data(), logt.data(), jump.data()};
+    a.grec = grec.data();
     a.segsum = segsum.data();
     a.segcnt = segcnt.data();
     a.nslow = nslow.data();

@@ -149,7 +149,7 @@ void run_caps(int caps, const int64_t *prop, const uint32_t *sids, HostSrc &src,
         if (ok) {
             if (caps == 10) run_mixed<M, NS, 2, 4, 2, 4>(prop, sids, src, D, o);
             else if (caps == 11) run_mixed<M, NS, 1, 2, 1, 4>(prop, sids, src, D, o);
-            else run_mixed<M, NS, 1, 1, 1, 6>(prop, sids, src, D, o);
+            else run_mixed<M, NS, 1, 4, 1, 4>(prop, sids, src, D, o);
             return;
         }
         caps -= 10;
