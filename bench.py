@@ -30,9 +30,15 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 
 
 # HBM bytes per launch of the dominant kernel at the default run counts, from rocprofv3 PMC passes
-# (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, separate passes; profiles/r01/pmc_f1.md).
-# PMC counters cannot be collected inside this process; these are the recorded values of the same command.
-TRAFFIC_PMC = {("c2", 32768): 7.363e9, ("c5", 65536): 9.128e8}
+# (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, separate passes; c2: profiles/r02/pmc_q.md, K1
+# without the per-block word stream; c5: profiles/r01/pmc_f1.md). PMC counters cannot be collected inside
+# this process; these are the recorded values of the same command.
+TRAFFIC_PMC = {("c2", 32768): 4.09e8, ("c5", 65536): 9.128e8}
+TRAFFIC_SRC = {"c2": "profiles/r02/pmc_q.md", "c5": "profiles/r01/pmc_f1.md"}
+# SQ_INSTS_VALU (wave instructions) per launch of the kernels the live timing covers, same passes
+# (c2: K1 only, timed by k1_ms; c3: D1 + E1 = the whole launch, timed by kernel_ms): the counter-based
+# VALU issue fraction = instructions x 64 lanes / time / peak, reported beside the SURVEY 8(d) convention.
+VALU_INSTS_PMC = {("c2", 32768): (2.269e9, "k1"), ("c3", 131072): (8.241e9 + 2.794e10, "launch")}
 
 
 def w_blk(m: int) -> int:
@@ -111,6 +117,7 @@ def main() -> None:
     ap.add_argument("--runs", type=int, default=0,
                     help="runs per GPU per step (0: 32768 = SIM_RUNS; c3: 131072 = configs[2]'s 1M runs / 8 GPUs; c5: 65536)")
     ap.add_argument("--seed-base", type=int, default=1000)
+    ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps alternate over (1: serial)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
     args = ap.parse_args()
@@ -134,26 +141,40 @@ def main() -> None:
     sim = Simulation(miners, total_weight=PRESET_WEIGHTS.get(args.config, 100))
     n = args.runs or {"c3": 131072, "c5": 65536}.get(args.config, 32768)
     dev = torch.device("cuda", local)
-    ws = torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev)
-    sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
-    total = torch.zeros((m, 6), dtype=torch.int64, device=dev)
-    status = torch.zeros(2, dtype=torch.int32, device=dev)
-    fails = torch.zeros(1, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # Consecutive steps are independent batches: they alternate over `--streams` HIP streams, each with its
+    # own workspace and sums, so one step's latency-bound tail kernels (episodes, combine, finalize) and
+    # all-reduce overlap the next step's draw kernel. Every step still runs to completion inside the timed
+    # region (both sides bracketed by barrier + synchronize).
+    ns = max(1, args.streams)
+    lanes = []
+    for j in range(ns):
+        st = torch.cuda.current_stream(dev) if ns == 1 else torch.cuda.Stream(dev)
+        lanes.append({
+            "stream": st,
+            "ws": torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev),
+            "sums": torch.zeros((m, 6), dtype=torch.int64, device=dev),
+            "total": torch.zeros((m, 6), dtype=torch.int64, device=dev),
+            "status": torch.zeros(2, dtype=torch.int32, device=dev),
+            "fails": torch.zeros(1, dtype=torch.int64, device=dev),
+        })
+    torch.cuda.synchronize()
 
     def step(i: int):
         begin = (i * world + rank) * n  # disjoint run ranges per step and rank -> fresh seeds
-        sim.launch(n, begin, args.seed_base, sums, ws, status, stream=stream)
-        fails.add_(status[1:2].to(torch.int64))
-        if world > 1:
-            dist.all_reduce(sums)  # the path's only exchange: per-miner integer sums (RCCL over xGMI)
-        total.add_(sums)
+        ln = lanes[i % ns]
+        with torch.cuda.stream(ln["stream"]):
+            sim.launch(n, begin, args.seed_base, ln["sums"], ln["ws"], ln["status"], stream=ln["stream"])
+            ln["fails"].add_(ln["status"][1:2].to(torch.int64))
+            if world > 1:
+                dist.all_reduce(ln["sums"])  # the path's only exchange: per-miner integer sums (RCCL over xGMI)
+            ln["total"].add_(ln["sums"])
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    total.zero_()
-    fails.zero_()
+    for ln in lanes:
+        ln["total"].zero_()
+        ln["fails"].zero_()
     timing_enable(True)  # HIP events on the launch stream around every launch and every K1
     if world > 1:
         dist.barrier()
@@ -170,6 +191,8 @@ def main() -> None:
     assert tm["launches"] == args.steps, tm
     kern_ms = tm["launch_ms"] / args.steps  # all kernels of one msim_launch (K1+K2+K3+finalize)
     k1_ms = tm["draws_ms"] / args.steps
+    total = sum(ln["total"] for ln in lanes)
+    fails = sum(ln["fails"] for ln in lanes)
     t = torch.tensor([elapsed, kern_ms, k1_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -179,6 +202,13 @@ def main() -> None:
         raise SystemExit(f"{int(fails.item())} runs exceeded the compact state capacity")
 
     pipe = sim.pipeline_info(n)
+    issue_frac, issue_src = None, None
+    if (args.config, n) in VALU_INSTS_PMC:
+        insts, which = VALU_INSTS_PMC[(args.config, n)]
+        t_s = (k1_ms if which == "k1" else kern_ms) / 1e3
+        issue_frac = round(insts * 64 / t_s / VALU_PEAK_LANE_OPS, 4) if t_s > 0 else None
+        issue_src = (f"SQ_INSTS_VALU {insts:.4g} per launch (profiles/r02/pmc_q.md) x 64 lanes / live "
+                     f"{'K1' if which == 'k1' else 'launch'} time / peak")
     runs_total = args.steps * n * world
     value = runs_total / elapsed
     per_gpu_kernel_rate = n / (kern_ms / 1e3)  # run-years/s of one launch on one GPU
@@ -208,7 +238,8 @@ def main() -> None:
                             f"{m} miners: weights 30720, 29696, 1024 x 41 (W=102400), all honest, prop 1000 ms"),
                 "runs_per_gpu_per_step": n,
                 "duration": "months{12} = 31556952000 ms",
-                "parallelism": f"runs sharded over {world} GPU(s), RCCL all-reduce of per-miner integer sums",
+                "parallelism": f"runs sharded over {world} GPU(s), RCCL all-reduce of per-miner integer sums; "
+                               f"steps alternate over {ns} HIP stream(s)",
                 "miner0_share_pct": round(share0, 5),
             },
             "roofline": {
@@ -219,8 +250,10 @@ def main() -> None:
                 "frac": round(achieved / VALU_PEAK_LANE_OPS, 5),
                 "traffic": TRAFFIC_PMC.get((args.config, n)),
                 "traffic_source": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this command, recorded in "
-                                   "profiles/r01/pmc_f1.md (bytes per launch of the draw kernel)")
+                                   f"{TRAFFIC_SRC.get(args.config)} (bytes per launch of the draw kernel)")
                 if (args.config, n) in TRAFFIC_PMC else None,
+                "valu_issue_frac_pmc": issue_frac,
+                "valu_issue_source": issue_src,
                 "kernel": ("msim_launch = W1 msim_wide_draws_kernel + W2 episodes + W3 combine" if sim.wide else
                            "msim_launch = K1 msim_draws_kernel + K2 episodes + K3 combine + finalize") +
                           " (HIP events on the launch stream; conservative: the whole launch, not the draw kernel alone)",
