@@ -459,9 +459,9 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
         if (v[i]) atomicAdd((unsigned long long *)(a.retry_sums + (size_t)point * 6 * M + i), (unsigned long long)v[i]);
 }
 
-// One capacity class (2 hot active slots, 4 reveal groups, 2 in-flight blocks per hot slot, SEL_NC cold
-// slots) for every network: measured on the 360-point configs[3] sweep, a wider register class (3, 8, 3)
-// spilled and ran the whole sweep 2.1x slower than this one, which flagged no run.
+// Capacity classes (msim_sel_launch.h). Measured on the 360-point configs[3] grid: with one selfish miner the
+// (1 hot slot, 2 reveal groups) class flagged ~1 % of the runs (reveal groups) and (1, 4) none; the engine
+// alone with a wider register class (3, 8, 3) spilled and ran the sweep 2.1x slower than (2, 4, 2).
 template <int M, int NS>
 static hipError_t launch_sel_ns(const SelArgs &a, hipStream_t s)
 {

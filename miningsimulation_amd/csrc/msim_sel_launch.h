@@ -25,9 +25,10 @@ namespace msim {
 
 constexpr uint32_t SEL_TILE = 32;  // words per (run, tile)
 
-// Capacities of E1: 2 hot active slots, 4 reveal groups, 2 in-flight blocks per hot active slot, backed
-// by SEL_NC cold slots in global memory (msim_sel.h). A run that exceeds them anyway is recomputed by E2,
-// which costs a whole run-year on one lane, so E1 must practically never flag.
+// Capacities of E1: one selfish miner (the mixed schedule): 1 hot active slot, 4 reveal groups, 1 in-flight
+// block per hot slot; several selfish miners (the engine alone): 2 / 4 / 2. Both are backed by SEL_NC cold
+// slots in global memory (msim_sel.h). A run that exceeds them anyway is recomputed by E2 (wide capacities,
+// one lane per run), so E1 must practically never flag: no run of configs[2] / configs[3] does.
 constexpr int SEL_NC = 4;
 
 // One network of a launch (a sweep point).
