@@ -9,6 +9,9 @@
 
 namespace msim {
 
+#ifndef SEL_LUT
+#define SEL_LUT 1  // word code -> finder through a 128-entry LDS table (one read instead of M compares)
+#endif
 #ifndef SEL_WAVES
 #define SEL_WAVES 2  // E1 occupancy target (waves per SIMD): 256 VGPRs, no spills
 #endif
@@ -51,12 +54,20 @@ struct SelWordSrc {
     uint4 pend;      // load in flight (when hp)
     bool hn, hp;
     uint32_t nl;     // block index of the next load
+#if SEL_LUT
+    const uint8_t *lut;  // finder of every code (LDS, built per workgroup from the point's thresholds)
+#else
     uint32_t cc[M];  // finder = #{k : cc[k] <= code} (the point's thresholds, msim_sel_launch.h)
+#endif
     __device__ __forceinline__ uint4 ld(uint32_t c) const { return p[(size_t)(c / SEL_TILE) * row + ((c % SEL_TILE) >> 2)]; }
     __device__ __forceinline__ void init(const uint32_t *ccum)
     {
 #pragma unroll
-        for (int j = 0; j < M; ++j) cc[j] = __builtin_amdgcn_readfirstlane(ccum[j]);  // wave-uniform: SGPRs
+        for (int j = 0; j < M; ++j) {
+#if !SEL_LUT
+            cc[j] = __builtin_amdgcn_readfirstlane(ccum[j]);  // wave-uniform: SGPRs
+#endif
+        }
         b = 0;
         const uint4 x = ld(0);
         c0 = x.x;
@@ -102,10 +113,14 @@ struct SelWordSrc {
         const uint32_t w = c0;
         I = w >> 7;
         const uint32_t q = w & 127u;
+#if SEL_LUT
+        k = lut[q];  // >= m: PickFinder falls through (simulation.h:220)
+#else
         uint32_t f = 0;
 #pragma unroll
         for (int j = 0; j < M; ++j) f += cc[j] <= q ? 1u : 0u;
         k = f;  // >= m: PickFinder falls through (simulation.h:220)
+#endif
         return true;
     }
     __device__ __forceinline__ void pop()
@@ -354,11 +369,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
     __shared__ uint32_t s_cnt[4 * M][TPB];
     __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
     __shared__ int64_t s_prop[MAXM];
+    __shared__ uint8_t s_lut[128];
     const uint32_t tid = threadIdx.x;
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
     const uint32_t point = a.plist[blockIdx.x / wps], blk = blockIdx.x % wps;
     const SelParams *P = a.pts + point;
     if (tid < MAXM) s_prop[tid] = P->prop[tid];
+    if (tid < 128) {
+        uint32_t f = 0;
+        for (int j = 0; j < MAXM; ++j) f += P->ccum[j] <= tid ? 1u : 0u;
+        s_lut[tid] = (uint8_t)f;
+    }
 #pragma unroll
     for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
     __syncthreads();
@@ -375,6 +396,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         src.p = reinterpret_cast<const uint4 *>(a.words) + (size_t)lr * (SEL_TILE / 4);
         src.row = (size_t)a.nr * (SEL_TILE / 4);
         src.nb = a.nb;
+#if SEL_LUT
+        src.lut = s_lut;
+#endif
         src.init(P->ccum);
         SelOut o;
         const int64_t D = P->duration_ms;
