@@ -131,6 +131,14 @@ struct SelWordSrc {
         --left;
         ++b;
     }
+    __device__ __forceinline__ void pop_if(bool p)  // pop() without a branch
+    {
+        c0 = p ? c1 : c0;
+        c1 = p ? c2 : c1;
+        c2 = p ? c3 : c2;
+        left -= p ? 1u : 0u;
+        b += p ? 1u : 0u;
+    }
     __device__ __forceinline__ bool next(uint32_t &I, uint32_t &k)
     {
         if (!peek(I, k)) return false;
@@ -174,6 +182,7 @@ struct SelRngSrc {
         return true;
     }
     __device__ void pop() { held = false; }
+    __device__ void pop_if(bool p) { held = held && !p; }
     __device__ void prefetch() {}
     __device__ void settle() {}
 };

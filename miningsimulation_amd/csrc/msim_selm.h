@@ -108,12 +108,17 @@ struct SelMacro {
         const bool have = src.peek(I, kn);
         const bool is_s = k == sid;
         const int64_t thr = is_s ? 0 : env.prop(k) + (w != 0u ? ps : 0);
-        const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (is_s | (((int64_t)I > thr) & (T + thr < D)));
-        if (!ok) return 1;
-        const bool hon = !is_s;
+        // (F - Ff bounds the honest stale blocks added to stp since the last flush: a lane about to reach
+        // 2^16 takes the engine path, whose hand-over flushes)
+        const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (F - Ff < 0xFF00u) &
+                        (is_s | (((int64_t)I > thr) & (T + thr < D)));
+        // Branch-free: a lane that needs the engine applies nothing (every update below is masked by ok).
+        const bool hon = ok & !is_s;
+        const bool sf = ok & is_s;
         const bool res = hon & (w == 0u);     // the honest branch wins (h == 0: a plain honest block)
         const bool swin = hon & (w == 2u);    // the selfish branch wins
         const bool tie = hon & !res & !swin;  // one more tied block each
+        const bool rs = res | swin;
         // k's block joins the honest branch (a resolving branch is cleared below)
         const uint32_t inc = hon ? 1u << (16 * (k & 1u)) : 0u;
 #pragma unroll
@@ -122,16 +127,15 @@ struct SelMacro {
         for (int i = 0; i < NPW; ++i) stp[i] += swin ? pend[i] : 0u;
         sst += res ? h : 0u;
         F += res ? h + 1u : (swin ? h + 2u : 0u);
-        h = (res | swin) ? 0u : h + (tie ? 1u : 0u);
-        w = is_s ? w + 1u : ((res | swin) ? 0u : w - 1u);
+        h = rs ? 0u : h + (tie ? 1u : 0u);
+        w = sf ? w + 1u : (rs ? 0u : w - (tie ? 1u : 0u));
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) pend[i] = (res | swin) ? 0u : pend[i];
-        env.add(C_F, k, 1u);
-        if (F - Ff >= 0xFF00u) flush_stale(env, sid);
-        src.pop();
-        T += (int64_t)I;
-        k = kn;
-        return T < D ? 0 : 2;
+        for (int i = 0; i < NPW; ++i) pend[i] = rs ? 0u : pend[i];
+        env.add(C_F, k < (uint32_t)M ? k : 0u, ok ? 1u : 0u);
+        src.pop_if(ok);
+        T += ok ? (int64_t)I : 0;
+        k = ok ? kn : k;
+        return ok ? (T < D ? 0 : 2) : 1;
     }
 
     template <class Env>

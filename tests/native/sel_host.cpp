@@ -50,6 +50,7 @@ struct HostSrc {
         return true;
     }
     void pop() { held = false; }
+    void pop_if(bool p) { held = held && !p; }
     bool next(uint32_t &I, uint32_t &k)
     {
         peek(I, k);
