@@ -38,7 +38,8 @@ TRAFFIC_SRC = {"c2": "profiles/r02/pmc_q.md", "c5": "profiles/r01/pmc_f1.md"}
 # SQ_INSTS_VALU (wave instructions) per launch of the kernels the live timing covers, same passes
 # (c2: K1 only, timed by k1_ms; c3: D1 + E1 = the whole launch, timed by kernel_ms): the counter-based
 # VALU issue fraction = instructions x 64 lanes / time / peak, reported beside the SURVEY 8(d) convention.
-VALU_INSTS_PMC = {("c2", 32768): (2.269e9, "k1"), ("c3", 131072): (8.241e9 + 2.794e10, "launch")}
+VALU_INSTS_PMC = {("c2", 32768): (2.269e9, "k1"), ("c3", 131072): (8.241e9 + 2.350e10, "launch"),
+                  ("c5", 65536): (5.81e9, "k1")}
 
 
 def w_blk(m: int) -> int:
@@ -207,11 +208,17 @@ def main() -> None:
         insts, which = VALU_INSTS_PMC[(args.config, n)]
         t_s = (k1_ms if which == "k1" else kern_ms) / 1e3
         issue_frac = round(insts * 64 / t_s / VALU_PEAK_LANE_OPS, 4) if t_s > 0 else None
-        issue_src = (f"SQ_INSTS_VALU {insts:.4g} per launch (profiles/r02/pmc_q.md) x 64 lanes / live "
+        issue_src = (f"SQ_INSTS_VALU {insts:.4g} per launch (profiles/r02/pmc_q.md, counters_s.md) x 64 lanes / live "
                      f"{'K1' if which == 'k1' else 'launch'} time / peak")
     runs_total = args.steps * n * world
     value = runs_total / elapsed
-    per_gpu_kernel_rate = n / (kern_ms / 1e3)  # run-years/s of one launch on one GPU
+    # Roofline of the dominant kernel: the draw kernel (K1 / W1) for honest networks, which does every fast
+    # block's whole work; for selfish networks the whole launch (D1 draws + E1 engine). Live HIP-event time
+    # on the launch stream; with --streams 2 a launch shares the GPU with the other stream's, so this
+    # duration (and rocprof's, which agrees) is longer than the kernel alone.
+    honest = pipe.get("uses_pipeline") in (1, 2)
+    dom_ms = k1_ms if honest and k1_ms > 0 else kern_ms
+    per_gpu_kernel_rate = n / (dom_ms / 1e3)  # run-years/s of the dominant kernel on one GPU
     achieved = per_gpu_kernel_rate * BLOCKS_PER_RUN_YEAR * w_blk(m)  # algorithmic lane-ops/s per GPU
     # sanity: aggregate share of miner 0 (integer sums, exact across ranks)
     tot = total.cpu().tolist()
@@ -254,9 +261,10 @@ def main() -> None:
                 if (args.config, n) in TRAFFIC_PMC else None,
                 "valu_issue_frac_pmc": issue_frac,
                 "valu_issue_source": issue_src,
-                "kernel": ("msim_launch = W1 msim_wide_draws_kernel + W2 episodes + W3 combine" if sim.wide else
-                           "msim_launch = K1 msim_draws_kernel + K2 episodes + K3 combine + finalize") +
-                          " (HIP events on the launch stream; conservative: the whole launch, not the draw kernel alone)",
+                "kernel": ("W1 msim_wide_draws_kernel" if sim.wide else "K1 msim_draws_kernel" if honest else
+                           "msim_launch = D1 msim_word_draws_kernel + E1 msim_sel_kernel + E2 retries + finalize") +
+                          " (HIP events on the launch stream)",
+                "dominant_ms": round(dom_ms, 4),
                 "kernel_ms": round(kern_ms, 4),
                 "k1_ms": round(k1_ms, 4),
                 "k1_share": round(k1_ms / kern_ms, 4) if kern_ms > 0 else None,
