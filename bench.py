@@ -118,7 +118,9 @@ def main() -> None:
     ap.add_argument("--runs", type=int, default=0,
                     help="runs per GPU per step (0: 32768 = SIM_RUNS; c3: 131072 = configs[2]'s 1M runs / 8 GPUs; c5: 65536)")
     ap.add_argument("--seed-base", type=int, default=1000)
-    ap.add_argument("--streams", type=int, default=2, help="HIP streams the steps alternate over (1: serial)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="HIP streams the steps alternate over (1: serial; 0: 2 for honest networks, whose "
+                         "latency-bound tail kernels overlap the next draw kernel, 1 for selfish ones)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
     args = ap.parse_args()
@@ -146,7 +148,7 @@ def main() -> None:
     # own workspace and sums, so one step's latency-bound tail kernels (episodes, combine, finalize) and
     # all-reduce overlap the next step's draw kernel. Every step still runs to completion inside the timed
     # region (both sides bracketed by barrier + synchronize).
-    ns = max(1, args.streams)
+    ns = args.streams if args.streams > 0 else (2 if sim.pipeline_info(n).get("uses_pipeline") in (1, 2) else 1)
     lanes = []
     for j in range(ns):
         st = torch.cuda.current_stream(dev) if ns == 1 else torch.cuda.Stream(dev)
