@@ -316,3 +316,37 @@ def test_host_dropin_driver_sweep(msim, tmp_path):
         rows = [[s.blocks_found, s.stale_blocks, s.share_hi, s.share_lo, s.rate_hi, s.rate_lo] for s in r.sums]
         want += msim.report(g, msim.sums_to_stats(rows), 512).splitlines()
     assert out == want
+
+
+@pytest.mark.parametrize("preset", ["c2", "c3"])
+def test_gpu_overlapped_streams_equal_serial(msim, preset):
+    """bench.py overlaps consecutive steps on two HIP streams (each with its own workspace): launches in
+    flight together give exactly the sums of the same launches run one after the other."""
+    import torch
+
+    sim = msim.Simulation(msim.PRESETS[preset]())
+    m = len(sim.miners)
+    n = 8192
+    dev = torch.device("cuda", 0)
+    lanes = [(torch.cuda.Stream(dev), torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev),
+              torch.zeros((m, 6), dtype=torch.int64, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
+              torch.zeros((m, 6), dtype=torch.int64, device=dev)) for _ in range(2)]
+    torch.cuda.synchronize()
+    for i in range(4):  # steps i and i+1 are in flight together
+        st, ws, sums, status, acc = lanes[i % 2]
+        with torch.cuda.stream(st):
+            sim.launch(n, i * n, 1000, sums, ws, status, stream=st)
+            acc.add_(sums)  # ordered on st after its own launch
+    torch.cuda.synchronize()
+    got = lanes[0][4] + lanes[1][4]
+    assert int(lanes[0][3][1]) == 0 and int(lanes[1][3][1]) == 0
+    want = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+    ws = torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev)
+    sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+    status = torch.zeros(2, dtype=torch.int32, device=dev)
+    for i in range(4):
+        sim.launch(n, i * n, 1000, sums, ws, status)
+        want.add_(sums)
+        assert int(status[1]) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
