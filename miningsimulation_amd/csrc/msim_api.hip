@@ -361,6 +361,13 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
     for (uint32_t k = 0; k < n; ++k)
         if (miners[k].propagation_ms < 1) sp->macro = 0;
     if (getenv("MSIM_SEL_NO_MACRO")) sp->macro = 0;  // A/B switch: the entity engine for every find
+    // Engine phases start when this many lanes of a wave wait. Long delays send more finds to the engine,
+    // and larger batches then pay (measured on MI355X, SEL_XTH A/B: configs[2] at 1 s fastest with 16, the
+    // configs[3] grid up to 30 s with 32; profiles/r02/xth_v.txt).
+    int64_t pmax = 0;
+    for (uint32_t k = 0; k < n; ++k) pmax = miners[k].propagation_ms > pmax ? miners[k].propagation_ms : pmax;
+    sp->xth = pmax <= 2000 ? 16u : 32u;
+    if (const char *e = getenv("MSIM_SEL_XTH")) sp->xth = (uint32_t)atoi(e);  // A/B override
 }
 
 struct SelGroupDev {

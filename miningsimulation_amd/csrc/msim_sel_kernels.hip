@@ -209,7 +209,7 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 }
 
 // The mixed schedule of a network with one selfish miner (msim_selm.h): every lane runs the settled-state
-// form until one of its finds needs the entity engine, then waits; when SEL_XTH lanes wait (or no lane is
+// form until one of its finds needs the entity engine, then waits; when P->xth lanes wait (or no lane is
 // left in the settled form) the wave runs an engine phase: the waiting lanes enter the engine, which steps
 // every one of them until it hands its run back (episodes are short: 5-6 events on average, 13 at the
 // 99th percentile over the configs[3] grid) or finishes it. The engine's state exists only inside a phase,
@@ -245,6 +245,7 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
     const uint32_t sid = P->sids[0];
     const int64_t ps = P->prop[sid];
     const bool mac = P->macro != 0u;  // wave-uniform (one point per workgroup)
+    const int xth = (int)__builtin_amdgcn_readfirstlane(P->xth >= 1u && P->xth <= 64u ? P->xth : (uint32_t)SEL_XTH);
     int mode = 0;
     if (!mac) {  // the entity engine for every find
         mode = 1;
@@ -267,9 +268,9 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
         if ((bm | be) == 0ull) break;
 #if SEL_PROF
         const uint64_t pc0 = clock64();
-        const bool pexact = be != 0ull && (__builtin_popcountll(be) >= SEL_XTH || bm == 0ull);
+        const bool pexact = be != 0ull && (__builtin_popcountll(be) >= xth || bm == 0ull);
 #endif
-        if (be != 0ull && (__builtin_popcountll(be) >= SEL_XTH || bm == 0ull)) {
+        if (be != 0ull && (__builtin_popcountll(be) >= xth || bm == 0ull)) {
             SelT s;
             if (mode == 1) {
                 if (mac) {
@@ -340,7 +341,7 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
                 pl_m += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 0));
 #endif
                 if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
-                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 1)) >= SEL_XTH)
+                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 1)) >= xth)
                     break;
             }
         }

@@ -47,6 +47,8 @@ struct SelParams {
     // carry the finder and ccum[k] = k + 1. Unused entries 0xFFFFFFFF; a result >= m falls through.
     uint32_t ccum[MAXM];
     uint32_t macro;      // 1: one selfish miner, every propagation >= 1 ms (the settled form applies, msim_selm.h)
+    uint32_t xth;        // waiting lanes that start an engine phase (mixed schedule, msim_sel_kernels.hip)
+    uint32_t pad3;
 };
 
 struct WordArgs {
