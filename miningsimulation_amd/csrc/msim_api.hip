@@ -366,7 +366,7 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
     // configs[3] grid up to 30 s with 32; profiles/r02/xth_v.txt).
     int64_t pmax = 0;
     for (uint32_t k = 0; k < n; ++k) pmax = miners[k].propagation_ms > pmax ? miners[k].propagation_ms : pmax;
-    sp->xth = pmax <= 2000 ? 16u : 32u;
+    sp->xth = pmax <= 2000 ? 16u : (pmax <= 10000 ? 32u : 48u);
     if (const char *e = getenv("MSIM_SEL_XTH")) sp->xth = (uint32_t)atoi(e);  // A/B override
 }
 
