@@ -223,6 +223,9 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #ifndef SEL_PROF
 #define SEL_PROF 0
 #endif
+#ifndef SEL_MSTEPS
+#define SEL_MSTEPS 2
+#endif
 #ifndef SEL_MC_LDS
 #define SEL_MC_LDS 1  // the settled-form state waits in LDS during engine phases
 #endif
@@ -324,16 +327,20 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
 #endif
         } else {
             for (;;) {
-                if (mode == 0) {
-                    src.prefetch();  // consumed at a later refill (peek settles only when it must)
-                    const int r = mc.step(env, src, D, sid, ps);
-                    if (r == 2) {
-                        SelOut q;
-                        mc.finish(env, sid, q);
-                        park(q);
-                        mode = 3;
-                    } else if (r == 1) {
-                        mode = 1;
+                // SEL_MSTEPS settled-form steps per exit test (a lane that leaves the form skips the rest)
+#pragma unroll
+                for (int u = 0; u < SEL_MSTEPS; ++u) {
+                    if (mode == 0) {
+                        src.prefetch();  // consumed at a later refill (peek settles only when it must)
+                        const int r = mc.step(env, src, D, sid, ps);
+                        if (r == 2) {
+                            SelOut q;
+                            mc.finish(env, sid, q);
+                            park(q);
+                            mode = 3;
+                        } else if (r == 1) {
+                            mode = 1;
+                        }
                     }
                 }
 #if SEL_PROF
