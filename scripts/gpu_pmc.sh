@@ -1,11 +1,10 @@
 #!/bin/bash
-# Selfish A/B + phase profile (gpu_r2p.sh), then c2/c3 bench lines with 1 and 2 streams, and the PMC passes
-# of c2's draw kernel (traffic + instruction mix) for the bench line and DESIGN.
+# c2/c3 bench lines with 1 and 2 streams, and the PMC passes of c2's draw kernel (traffic + instruction
+# mix) behind the bench line's traffic and issue-fraction constants (profiles/r02/pmc_q.md).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r2q}; mkdir -p $O
-TAG=r2q_p bash scripts/gpu_r2p.sh || exit 1
+O=gpurun_out/${TAG:-pmc}; mkdir -p $O
 for c in c2 c3; do for st in 1 2; do
   timeout -k 10 300 python -u bench.py --config $c --streams $st --no-cpu-baseline > $O/bench_${c}_s$st.json 2> $O/bench_${c}_s$st.err || { tail -30 $O/bench_${c}_s$st.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/bench_${c}_s$st.json'));print('$c streams=$st',d['value'],d['ms_per_step'],d['roofline']['kernel_ms'],d['roofline']['k1_ms'])"

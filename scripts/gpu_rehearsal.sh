@@ -1,10 +1,10 @@
 #!/bin/bash
-# Final round-2 rehearsal of the committed code: full GPU suite, smoke, default bench (with CPU baseline),
+# Rehearsal of the committed code: full GPU suite, smoke, default bench (with CPU baseline),
 # c3 / c5 bench lines, the configs[3] sweep at 8192 runs/point.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r2y}; mkdir -p $O
+O=gpurun_out/${TAG:-rehearsal}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
