@@ -182,3 +182,18 @@ def test_gpu_c3_status_and_retry_rate(msim):
     one = sim.run(n, 0, 1000, 0)
     assert sums.cpu().numpy().tolist() == [[s.blocks_found, s.stale_blocks, s.share_hi, s.share_lo, s.rate_hi,
                                             s.rate_lo] for s in one.sums]
+
+
+@pytest.mark.parametrize("xth,no_macro", [(1, False), (64, False), (16, True)])
+def test_gpu_schedule_does_not_change_results(msim, monkeypatch, xth, no_macro):
+    """The mixed schedule only decides which lanes of a wave advance together (msim_sel_kernels.hip): any
+    engine-phase threshold, and the entity engine alone (no settled form), give the same per-run counters
+    as the default schedule on configs[2] (4 096 runs, a full year)."""
+    p, q, s = [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [1] + [0] * 8
+    base = _run(msim, p, q, s, 4096, begin=77)
+    monkeypatch.setenv("MSIM_SEL_XTH", str(xth))
+    if no_macro:
+        monkeypatch.setenv("MSIM_SEL_NO_MACRO", "1")
+    other = _run(msim, p, q, s, 4096, begin=77)
+    assert np.array_equal(base.found, other.found) and np.array_equal(base.stale, other.stale)
+    assert np.array_equal(base.best_height, other.best_height)
