@@ -8,6 +8,11 @@ Weak scaling: per-GPU work is fixed; each step and rank takes a fresh, disjoint 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--runs 32768]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL over xGMI)
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself (one child
+process per GPU, 127.0.0.1 rendezvous) before anything touches HIP, relays rank 0's JSON line and exits
+non-zero if any rank fails: the reference's own driver fans out over every hardware thread the same way
+(main.cpp:198-209).
+
 Rank 0 prints ONE JSON line (driver contract) with a live VALU roofline (HIP events around every launch
 on the launch stream) and, at N=1, the CPU baseline: the oracle (explicit-chain C port of the reference
 loop, oracle/msim_oracle.c) timed on a bounded sample on the host's cores.
@@ -69,31 +74,47 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def host_threads() -> tuple[int, str]:
-    """Every CPU this process may run on, bounded by the CPU share the host allots to one GPU job (the GPU
-    box exports OMP_NUM_THREADS = its per-GPU share; nproc there shows the whole machine)."""
+def host_threads() -> tuple[int, int, str]:
+    """(threads to use, visible CPUs, note). The GPU box exports OMP_NUM_THREADS = the CPU share one GPU
+    job may use (its nproc shows the whole machine); the harness asks worker pools to stay within that
+    share, so the timed sample uses it and the all-cores figure is extrapolated from it (cpu_baseline)."""
     cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     share = os.environ.get("OMP_NUM_THREADS")
     if share and share.isdigit() and 0 < int(share) < cpus:
-        return int(share), f"{share} of {cpus} visible CPUs (the host's per-GPU CPU share, OMP_NUM_THREADS)"
-    return cpus, f"all {cpus} visible CPUs"
+        return int(share), cpus, f"{share} of {cpus} visible CPUs (the job's CPU share, OMP_NUM_THREADS)"
+    return cpus, cpus, f"all {cpus} visible CPUs"
 
 
-def cpu_baseline(preset: str, sample_runs: int, threads: int, target_s: float = 15.0) -> dict:
+def cgroup_cpu_quota() -> str | None:
+    """cgroup v2 cpu.max of this process (quota period), if readable."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = f.read().strip().split("::")[-1]
+        with open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def cpu_baseline(preset: str, sample_runs: int, threads: int, visible: int, target_s: float = 15.0) -> dict:
+    """The oracle port (explicit chains like the reference) timed on `threads` host threads, plus a
+    one-thread sample (the per-core rate) and the all-visible-CPUs extrapolation of the threaded rate."""
     from oracle import pyoracle
 
     pyoracle.build()
 
-    def timed(runs: int) -> dict:
-        out = subprocess.run([pyoracle.CLI, "time", preset, str(runs), str(threads)], capture_output=True,
+    def timed(runs: int, th: int) -> dict:
+        out = subprocess.run([pyoracle.CLI, "time", preset, str(runs), str(th)], capture_output=True,
                              text=True, check=True)
         return json.loads(out.stdout.splitlines()[0])
 
+    per = 1 if preset == "c5" else 16  # c5: ~1 run-year/s per core (explicit chains, 1026 miners)
     if not sample_runs:  # calibrate on a small sample, then size the real sample to ~target_s seconds
-        per = 1 if preset == "c5" else 16  # c5: ~1 run-year/s per core (explicit chains, 1026 miners)
-        probe = timed(threads * per)
+        probe = timed(threads * per, threads)
         sample_runs = max(threads * per, int(probe["run_years_per_s"] * target_s) // threads * threads)
-    rec = timed(sample_runs)
+    rec = timed(sample_runs, threads)
+    one = timed(max(1, per // 2), 1)  # per-core rate (a few seconds)
+    per_thread = rec["run_years_per_s"] / threads
     return {
         "value": round(rec["run_years_per_s"], 2),
         "unit": "run-years/s",
@@ -102,11 +123,75 @@ def cpu_baseline(preset: str, sample_runs: int, threads: int, target_s: float = 
         "sample": f"{sample_runs} runs x 365.2425 d of preset {preset} (oracle/msim_oracle.c, explicit chains as "
                   f"in the reference, {threads} pthreads), {rec['seconds']:.1f} s wall",
         "cpu_model": cpu_model(),
+        "visible_cpus": visible,
+        "cgroup_cpu_max": cgroup_cpu_quota(),
+        "one_thread_value": round(one["run_years_per_s"], 3),
+        "all_visible_cpus_extrapolated": round(per_thread * visible, 1),
+        "all_cpus_note": f"{threads}-thread rate / {threads} x {visible} visible CPUs: the job may use only its "
+                         f"CPU share, so the whole-host figure is extrapolated (linear, an upper bound)",
         "port_to_reference_ratio": PORT_TO_REFERENCE,
         "reference_equivalent": round(rec["run_years_per_s"] / PORT_TO_REFERENCE, 2),
+        "reference_equivalent_all_visible_cpus": round(per_thread * visible / PORT_TO_REFERENCE, 1),
         "calibration": "port 352.1 vs reference binary 609 run-years/s, c2, 32768 runs, 8 threads, same container "
                        "(BASELINE.md §2); reference_equivalent = value / ratio",
     }
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Start ranks 0..n-1 of this script (one process per GPU) and relay rank 0's stdout. The parent never
+    imports torch or touches HIP: each child initialises its own device."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out = procs[0].communicate()[0]
+    codes = [procs[0].returncode]
+    for p in procs[1:]:
+        try:
+            codes.append(p.wait(timeout=120))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            codes.append(p.wait())
+    if any(c != 0 for c in codes):
+        print(f"bench.py: rank exit codes {codes}", file=sys.stderr)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        return 1
+    for ln in out.splitlines():  # the JSON line to stdout; library chatter (gloo/RCCL banners) to stderr
+        print(ln, file=sys.stdout if ln.startswith("{") else sys.stderr, flush=True)
+    return 0
+
+
+class _StubSim:
+    """--stub (tests only): a CPU stand-in for Simulation that fills deterministic integer sums, so the
+    rank spawn / gloo reduction / JSON path of this script runs without a GPU. Never used for a number."""
+
+    def __init__(self, m: int):
+        self.m, self.wide = m, False
+
+    def pipeline_info(self, n):
+        return {"uses_pipeline": 1, "stub": 1}
+
+    def workspace_bytes(self, n):
+        return 8
+
+    def launch(self, n, begin, seed_base, sums, ws, status, stream=None):
+        import torch
+
+        sums.copy_(torch.arange(sums.numel(), dtype=torch.int64).reshape(sums.shape) + n)
+        status.zero_()
 
 
 def main() -> None:
@@ -123,7 +208,13 @@ def main() -> None:
                          "latency-bound tail kernels overlap the next draw kernel, 1 for selfish ones)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # tests: CPU stand-in, gloo
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:]))
+
+    import contextlib
 
     import torch
     import torch.distributed as dist
@@ -131,19 +222,48 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.stub:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=dev)
 
-    from miningsimulation_amd import PRESETS, Simulation, timing_enable, timing_read
+    from miningsimulation_amd import PRESETS
     from miningsimulation_amd.simulation import PRESET_WEIGHTS
 
     miners = PRESETS[args.config]()
     m = len(miners)
-    sim = Simulation(miners, total_weight=PRESET_WEIGHTS.get(args.config, 100))
+    if args.stub:
+        sim = _StubSim(m)
+        stub_t = {"on": False}
+
+        def timing_enable(on):
+            stub_t["on"] = on
+
+        def timing_read():
+            return {"launches": args.steps, "launch_ms": 1.0 * args.steps, "draws_ms": 1.0 * args.steps}
+
+        def sync():
+            pass
+
+        def on_stream(st):
+            return contextlib.nullcontext()
+    else:
+        from miningsimulation_amd import Simulation, timing_enable, timing_read
+
+        sim = Simulation(miners, total_weight=PRESET_WEIGHTS.get(args.config, 100))
+
+        def sync():
+            torch.cuda.synchronize()
+
+        def on_stream(st):
+            return torch.cuda.stream(st)
     n = args.runs or {"c3": 131072, "c5": 65536}.get(args.config, 32768)
-    dev = torch.device("cuda", local)
     # Consecutive steps are independent batches: they alternate over `--streams` HIP streams, each with its
     # own workspace and sums, so one step's latency-bound tail kernels (episodes, combine, finalize) and
     # all-reduce overlap the next step's draw kernel. Every step still runs to completion inside the timed
@@ -151,7 +271,7 @@ def main() -> None:
     ns = args.streams if args.streams > 0 else (2 if sim.pipeline_info(n).get("uses_pipeline") in (1, 2) else 1)
     lanes = []
     for j in range(ns):
-        st = torch.cuda.current_stream(dev) if ns == 1 else torch.cuda.Stream(dev)
+        st = None if args.stub else (torch.cuda.current_stream(dev) if ns == 1 else torch.cuda.Stream(dev))
         lanes.append({
             "stream": st,
             "ws": torch.empty(sim.workspace_bytes(n), dtype=torch.uint8, device=dev),
@@ -160,12 +280,12 @@ def main() -> None:
             "status": torch.zeros(2, dtype=torch.int32, device=dev),
             "fails": torch.zeros(1, dtype=torch.int64, device=dev),
         })
-    torch.cuda.synchronize()
+    sync()
 
     def step(i: int):
         begin = (i * world + rank) * n  # disjoint run ranges per step and rank -> fresh seeds
         ln = lanes[i % ns]
-        with torch.cuda.stream(ln["stream"]):
+        with on_stream(ln["stream"]):
             sim.launch(n, begin, args.seed_base, ln["sums"], ln["ws"], ln["status"], stream=ln["stream"])
             ln["fails"].add_(ln["status"][1:2].to(torch.int64))
             if world > 1:
@@ -174,18 +294,18 @@ def main() -> None:
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
+    sync()
     for ln in lanes:
         ln["total"].zero_()
         ln["fails"].zero_()
     timing_enable(True)  # HIP events on the launch stream around every launch and every K1
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -274,9 +394,11 @@ def main() -> None:
                 "accounting": f"SURVEY 8(d): W_blk({m}) = {w_blk(m)} lane-ops/block x 52594.92 blocks/run-year",
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
-            threads, how = host_threads()
-            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_runs, threads)
+        if args.stub:
+            line["data"] = "STUB (--stub: CPU stand-in for the launch, tests of the rank/JSON plumbing only)"
+        if world == 1 and not args.no_cpu_baseline and not args.stub:
+            threads, visible, how = host_threads()
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample_runs, threads, visible)
             line["cpu_baseline"]["cores_note"] = how
         print(json.dumps(line), flush=True)
     if world > 1:

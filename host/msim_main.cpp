@@ -3,7 +3,7 @@
 // Keeps the reference's configuration surface unchanged — SIM_DURATION (main.cpp:7), SIM_RUNS
 // (main.cpp:10), SetupMiners() (main.cpp:44-65) with Miner(id, perc, propagation, selfish) — and its
 // report (main.cpp:201, 219-234). The std::async batch loop (main.cpp:205-220) is replaced by
-// msim_run_multi through the C ABI (include/msim.h): the runs are sharded over the GPUs, one host thread
+// msim_run_multi through the C ABI (include/msim.h): the runs are sharded over the GPUs, one stream
 // per GPU, and combined by one RCCL all-reduce of the integer sums.
 //
 // Sweeps (BASELINE configs[3]) — the reference edits SetupMiners and rebuilds per network
@@ -292,7 +292,7 @@ int main(int argc, char **argv)
     if (int rc = msim_config_create_weighted(desc.data(), (uint32_t)desc.size(), duration_ms, total_weight, &cfg))
         return die("config", rc);
 
-    // main.cpp:201 (one host thread drives each GPU)
+    // main.cpp:201 (the reference names its thread count; here one stream drives each GPU)
     std::printf("Running %d simulations in parallel using %d threads.\n", SIM_RUNS, n_gpus);
     std::vector<msim_stats> stats_total(miners.size());
     if (int rc = WithStdoutOnStderr([&] {

@@ -100,9 +100,11 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
 
 /* Several GPUs of one node (the std::async loop of main.cpp:205-220 across devices): runs
  * [run_begin, run_begin + n_runs) cut into contiguous shards, one per device in `devices` (NULL = devices
- * 0 .. n_devices - 1), each through msim_launch on its own host thread and stream, then ONE ncclAllReduce
- * (RCCL over xGMI, single-process communicator from ncclCommInitAll) of the integer msim_sums. The result
- * is bit-identical to msim_run for every n_devices (out_sums from the fixed-point sums; opt_sums or NULL). */
+ * 0 .. n_devices - 1), each through msim_launch on its own stream (all devices run concurrently), then ONE
+ * ncclAllReduce (RCCL over xGMI, single-process communicator from ncclCommInitAll, issued for every device
+ * inside one group) of the integer msim_sums. Every device's buffers are allocated before anything runs, so
+ * an allocation failure returns MSIM_E_HIP without entering a collective. The result is bit-identical to
+ * msim_run for every n_devices (out_sums from the fixed-point sums; opt_sums or NULL). */
 int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
                    const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums);
 

@@ -125,6 +125,7 @@ constexpr double PIPE_SLICE_BUDGET = 16.0 * (1ull << 30);  // pipeline workspace
 // K1 wave slots of the current device (CUs x resident K1 waves per CU); 8192 if it cannot be queried.
 uint32_t draw_slots()
 {
+    if (const char *e = getenv("MSIM_K1_SLOTS")) return (uint32_t)atoi(e);  // A/B override (measurement only)
     int dev = 0, cus = 0, blocks = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         msim::draws_blocks_per_cu(&blocks) != hipSuccess || cus <= 0 || blocks <= 0)

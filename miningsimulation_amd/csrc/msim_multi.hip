@@ -3,15 +3,14 @@
 //
 // The reference runs SIM_RUNS independent runs as std::async tasks and adds their MinerStats on the main
 // thread (main.cpp:209-217). Runs are independent and their seeds are a pure function of the run index,
-// so here the run range is cut into contiguous shards, one per device; each device's host thread runs its
-// shard through msim_launch (device-resident, its own stream), and the per-miner msim_sums (integers)
+// so here the run range is cut into contiguous shards, one per device; each device runs its shard
+// through msim_launch (device-resident, asynchronous on its own stream), and the per-miner msim_sums (integers)
 // are combined by ONE ncclAllReduce over a single-process communicator (ncclCommInitAll: RCCL over xGMI
 // on MI355X). Integer sums make the result bit-identical to msim_run for every device count.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
-#include <thread>
 #include <vector>
 
 #include "../../include/msim.h"
@@ -20,6 +19,7 @@ namespace {
 
 // runs per msim_launch on one device (as msim_run: keeps every launch's workspace bounded)
 constexpr uint64_t MULTI_CHUNK = 1ull << 22;
+constexpr uint64_t MAX_LAUNCH_RUNS = 1ull << 26;  // msim_launch / msim_sweep_launch limit (runs x points)
 
 __global__ void add_sums_kernel(uint64_t *acc, const uint64_t *part, uint32_t n)
 {
@@ -32,12 +32,18 @@ __global__ void add_status_kernel(uint32_t *acc, const uint32_t *part)
     if (threadIdx.x < 2) acc[threadIdx.x] += part[threadIdx.x];
 }
 
+// One device's shard and everything it needs, allocated before any launch or collective.
 struct Shard {
     int device;
-    uint64_t begin, n;
+    uint64_t begin, n, chunk;
+    size_t wsb = 0;
     int rc = MSIM_OK;
+    hipStream_t s = nullptr;
+    void *ws = nullptr;
     uint64_t *d_acc = nullptr;   // [nv] sums of every chunk (the all-reduce operand)
     uint32_t *d_stat = nullptr;  // [2] status of every chunk
+    uint64_t *d_part = nullptr;  // [nv] one chunk's sums
+    uint32_t *d_pst = nullptr;   // [2] one chunk's status
 };
 
 // What one device launches for a chunk of runs: a config (msim_launch) or a sweep (msim_sweep_launch).
@@ -45,6 +51,13 @@ struct Job {
     const msim_config *cfg;
     const msim_sweep *sweep;
     uint32_t nv;  // int64 values of the sums: 6 * M (config) or 6 * M * points (sweep)
+    // runs per launch: a sweep launch covers every point, so its limit is MAX_LAUNCH_RUNS / points
+    uint64_t max_chunk() const
+    {
+        if (cfg) return MULTI_CHUNK;
+        const uint64_t np = msim_sweep_point_count(sweep), c = np ? MAX_LAUNCH_RUNS / np : 1;
+        return c < 1 ? 1 : (c < MULTI_CHUNK ? c : MULTI_CHUNK);
+    }
     size_t ws_bytes(uint64_t n) const
     {
         return cfg ? msim_workspace_bytes(cfg, n) : msim_sweep_workspace_bytes(sweep, n);
@@ -57,51 +70,57 @@ struct Job {
     }
 };
 
-// One device: its shard in chunks, sums accumulated on the device, then the all-reduce.
-void run_shard(const Job &job, uint32_t seed_base, ncclComm_t comm, Shard &sh, hipStream_t *stream_out)
+int alloc_shard(const Job &job, Shard &sh)
+{
+    const uint32_t nv = job.nv;
+    const uint64_t mc = job.max_chunk();
+    sh.chunk = sh.n < mc ? sh.n : mc;
+    sh.wsb = sh.chunk ? job.ws_bytes(sh.chunk) : 0;
+    if (sh.chunk && sh.wsb == 0) return MSIM_E_INVALID;
+    if (hipSetDevice(sh.device) != hipSuccess || hipStreamCreate(&sh.s) != hipSuccess ||
+        hipMalloc(&sh.d_acc, nv * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&sh.d_stat, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&sh.d_part, nv * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&sh.d_pst, 2 * sizeof(uint32_t)) != hipSuccess || (sh.wsb && hipMalloc(&sh.ws, sh.wsb) != hipSuccess) ||
+        hipMemsetAsync(sh.d_acc, 0, nv * sizeof(uint64_t), sh.s) != hipSuccess ||
+        hipMemsetAsync(sh.d_stat, 0, 2 * sizeof(uint32_t), sh.s) != hipSuccess)
+        return MSIM_E_HIP;
+    return MSIM_OK;
+}
+
+void free_shard(Shard &sh)
+{
+    (void)hipSetDevice(sh.device);
+    (void)hipFree(sh.ws);
+    (void)hipFree(sh.d_part);
+    (void)hipFree(sh.d_pst);
+    (void)hipFree(sh.d_acc);
+    (void)hipFree(sh.d_stat);
+    if (sh.s) (void)hipStreamDestroy(sh.s);
+}
+
+// Enqueue one device's shard (asynchronous: every device runs its chunks concurrently on its stream).
+void enqueue_shard(const Job &job, uint32_t seed_base, Shard &sh)
 {
     if (hipSetDevice(sh.device) != hipSuccess) {
         sh.rc = MSIM_E_HIP;
         return;
     }
-    hipStream_t s = nullptr;
-    void *ws = nullptr;
-    uint64_t *d_part = nullptr;
-    uint32_t *d_pst = nullptr;
-    const uint32_t nv = job.nv;
-    const uint64_t chunk = sh.n < MULTI_CHUNK ? sh.n : MULTI_CHUNK;
-    const size_t wsb = chunk ? job.ws_bytes(chunk) : 0;
-    if (hipStreamCreate(&s) != hipSuccess || hipMalloc(&sh.d_acc, nv * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&sh.d_stat, 2 * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&d_part, nv * sizeof(uint64_t)) != hipSuccess || hipMalloc(&d_pst, 2 * sizeof(uint32_t)) != hipSuccess ||
-        (wsb && hipMalloc(&ws, wsb) != hipSuccess) ||
-        hipMemsetAsync(sh.d_acc, 0, nv * sizeof(uint64_t), s) != hipSuccess ||
-        hipMemsetAsync(sh.d_stat, 0, 2 * sizeof(uint32_t), s) != hipSuccess) {
-        sh.rc = MSIM_E_HIP;
-    }
-    for (uint64_t off = 0; sh.rc == MSIM_OK && off < sh.n; off += chunk) {
-        const uint64_t cn = (sh.n - off) < chunk ? (sh.n - off) : chunk;
-        sh.rc = job.launch(sh.begin + off, cn, seed_base, d_part, d_pst, ws, wsb, s);
+    for (uint64_t off = 0; sh.rc == MSIM_OK && off < sh.n; off += sh.chunk) {
+        const uint64_t cn = (sh.n - off) < sh.chunk ? (sh.n - off) : sh.chunk;
+        sh.rc = job.launch(sh.begin + off, cn, seed_base, sh.d_part, sh.d_pst, sh.ws, sh.wsb, sh.s);
         if (sh.rc) break;
-        hipLaunchKernelGGL(add_sums_kernel, dim3((nv + 255) / 256), dim3(256), 0, s, sh.d_acc, d_part, nv);
-        hipLaunchKernelGGL(add_status_kernel, dim3(1), dim3(64), 0, s, sh.d_stat, d_pst);
+        hipLaunchKernelGGL(add_sums_kernel, dim3((job.nv + 255) / 256), dim3(256), 0, sh.s, sh.d_acc, sh.d_part, job.nv);
+        hipLaunchKernelGGL(add_status_kernel, dim3(1), dim3(64), 0, sh.s, sh.d_stat, sh.d_pst);
         if (hipGetLastError() != hipSuccess) sh.rc = MSIM_E_HIP;
     }
-    // Every rank takes part in the collectives, also after a local error (a rank that skipped them would
-    // leave the others waiting): a failed shard contributes zeros and reports its own error code.
-    if (ncclGroupStart() != ncclSuccess ||
-        ncclAllReduce(sh.d_acc, sh.d_acc, nv, ncclUint64, ncclSum, comm, s) != ncclSuccess ||
-        ncclAllReduce(sh.d_stat, sh.d_stat, 2, ncclUint32, ncclSum, comm, s) != ncclSuccess ||
-        ncclGroupEnd() != ncclSuccess)
-        sh.rc = sh.rc ? sh.rc : MSIM_E_HIP;
-    if (hipStreamSynchronize(s) != hipSuccess) sh.rc = sh.rc ? sh.rc : MSIM_E_HIP;
-    (void)hipFree(ws);
-    (void)hipFree(d_part);
-    (void)hipFree(d_pst);
-    *stream_out = s;
 }
 
 // Shards [run_begin, run_begin + n_runs) over the devices, runs them, all-reduces; acc = reduced sums.
+// Every buffer of every device is allocated before anything is enqueued, and the collectives are issued
+// for all devices by this one thread inside one ncclGroupStart / ncclGroupEnd (the single-process
+// multi-device form), so no device can be left waiting in a collective that another never joins: a
+// device whose launches failed contributes its (zero-initialised) buffers and the call returns its error.
 int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, const int *devices,
             uint32_t n_devices, std::vector<uint64_t> &acc)
 {
@@ -111,27 +130,40 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
     if (hipGetDeviceCount(&count) != hipSuccess) return MSIM_E_HIP;
     for (int d : devs)
         if (d < 0 || d >= count) return MSIM_E_INVALID;
-    std::vector<ncclComm_t> comms(n_devices);
-    if (ncclCommInitAll(comms.data(), (int)n_devices, devs.data()) != ncclSuccess) return MSIM_E_HIP;
     // contiguous shards, as distributed.shard: the first n_runs % n_devices shards take one run more
     std::vector<Shard> sh(n_devices);
     const uint64_t base = n_runs / n_devices, rem = n_runs % n_devices;
+    int rc = MSIM_OK;
     for (uint32_t g = 0; g < n_devices; ++g) {
         sh[g].device = devs[g];
         sh[g].begin = run_begin + g * base + (g < rem ? g : rem);
         sh[g].n = base + (g < rem ? 1 : 0);
+        if (rc == MSIM_OK) rc = alloc_shard(job, sh[g]);
     }
-    std::vector<hipStream_t> streams(n_devices, nullptr);
-    std::vector<std::thread> th;
-    for (uint32_t g = 0; g < n_devices; ++g)
-        th.emplace_back(run_shard, std::cref(job), seed_base, comms[g], std::ref(sh[g]), &streams[g]);
-    for (auto &t : th) t.join();
-    int rc = MSIM_OK;
-    for (const auto &x : sh)
-        if (x.rc) rc = rc ? rc : x.rc;
+    std::vector<ncclComm_t> comms(n_devices, nullptr);
+    if (rc == MSIM_OK && ncclCommInitAll(comms.data(), (int)n_devices, devs.data()) != ncclSuccess) {
+        rc = MSIM_E_HIP;
+        comms.assign(n_devices, nullptr);
+    }
+    if (rc == MSIM_OK) {
+        for (auto &x : sh) enqueue_shard(job, seed_base, x);
+        if (ncclGroupStart() != ncclSuccess) {
+            rc = MSIM_E_HIP;
+        } else {
+            for (uint32_t g = 0; g < n_devices; ++g)
+                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv, ncclUint64, ncclSum, comms[g], sh[g].s) != ncclSuccess ||
+                    ncclAllReduce(sh[g].d_stat, sh[g].d_stat, 2, ncclUint32, ncclSum, comms[g], sh[g].s) != ncclSuccess)
+                    rc = MSIM_E_HIP;
+            if (ncclGroupEnd() != ncclSuccess) rc = MSIM_E_HIP;
+        }
+        for (auto &x : sh)
+            if (hipSetDevice(x.device) != hipSuccess || hipStreamSynchronize(x.s) != hipSuccess) rc = rc ? rc : MSIM_E_HIP;
+        for (const auto &x : sh)
+            if (x.rc) rc = rc ? rc : x.rc;
+    }
     acc.assign(job.nv, 0);
     uint32_t st[2] = {0, 0};
-    if (rc == MSIM_OK) {  // every rank holds the reduced sums: read the first device's
+    if (rc == MSIM_OK) {  // every device holds the reduced sums: read the first one's
         if (hipSetDevice(sh[0].device) != hipSuccess ||
             hipMemcpy(acc.data(), sh[0].d_acc, acc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(st, sh[0].d_stat, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess)
@@ -140,11 +172,8 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
             rc = MSIM_E_CAPACITY;
     }
     for (uint32_t g = 0; g < n_devices; ++g) {
-        (void)hipSetDevice(sh[g].device);
-        (void)hipFree(sh[g].d_acc);
-        (void)hipFree(sh[g].d_stat);
-        if (streams[g]) (void)hipStreamDestroy(streams[g]);
-        (void)ncclCommDestroy(comms[g]);
+        free_shard(sh[g]);
+        if (comms[g]) (void)ncclCommDestroy(comms[g]);
     }
     return rc;
 }

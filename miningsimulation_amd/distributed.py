@@ -60,12 +60,14 @@ MAX_LAUNCH_RUNS = 1 << 26  # msim_launch's per-call limit (msim_api.hip); larger
 
 
 def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=None,
-                launch: Optional[Callable] = None, device=None):
+                launch: Optional[Callable] = None, device=None, max_chunk: int = MAX_LAUNCH_RUNS):
     """This rank's shard through msim_launch on the current device, then one all-reduce (RCCL on GPUs).
 
     Returns the global [M, 6] int64 sums as a tensor on `device` (identical on every rank). `launch`
     replaces sim.launch (same signature, workspace None) so that the partition, chunking, status check and
     all-reduce can be exercised on CPU ranks with a gloo group (tests/test_distributed.py)."""
+    import contextlib
+
     import torch
     import torch.distributed as dist
 
@@ -78,18 +80,25 @@ def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=No
     status = torch.zeros(2, dtype=torch.int32, device=dev)
     part = torch.zeros_like(sums)
     pst = torch.zeros_like(status)
-    chunk = min(n, MAX_LAUNCH_RUNS)
+    chunk = min(n, max_chunk)
     ws = None
     if n and launch is None:
         ws = torch.empty(sim.workspace_bytes(chunk), dtype=torch.uint8, device=dev)
-    for off in range(0, n, max(chunk, 1)):
-        cn = min(chunk, n - off)
-        (launch or sim.launch)(cn, run_begin + begin + off, seed_base, part, ws, pst, stream=stream)
-        sums += part
-        status += pst
-    if world > 1:
-        dist.all_reduce(sums)
-        dist.all_reduce(status)
+    # Everything that touches the launch's outputs runs on the launch stream: the adds read `part` / `pst`
+    # after the kernels that wrote them, the next chunk's launch overwrites them only after the adds, and
+    # the all-reduce (RCCL enqueues on the current stream) sees the final sums.
+    ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
+    with ctx:
+        for off in range(0, n, max(chunk, 1)):
+            cn = min(chunk, n - off)
+            (launch or sim.launch)(cn, run_begin + begin + off, seed_base, part, ws, pst, stream=stream)
+            sums += part
+            status += pst
+        if world > 1:
+            dist.all_reduce(sums)
+            dist.all_reduce(status)
+    if stream is not None and dev.type == "cuda":
+        torch.cuda.current_stream(dev).wait_stream(stream)  # the caller's stream sees the result
     if int(status[1].item()) != 0:
         raise RuntimeError(f"{int(status[1].item())} runs exceeded the compact state capacity")
     return sums

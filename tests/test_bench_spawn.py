@@ -1,0 +1,37 @@
+"""bench.py --gpus N starts its own N ranks (one process per GPU, 127.0.0.1 rendezvous) when no launcher
+set WORLD_SIZE, and rank 0 prints the single JSON line of the whole job. Driven on CPU with --stub (gloo
+stand-in for the launch; the real path uses RCCL): the spawn, barrier, max-over-ranks and reduction
+plumbing is the same code."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--no-cpu-baseline", *args],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_spawn_two_ranks_one_line():
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1")
+    assert d["n_gpus"] == 2
+    assert d["steps"] == 3
+    assert d["scaling"] == "weak"
+    assert d["value"] > 0
+    assert d["data"].startswith("STUB")
+    # whole-job aggregate: 2 ranks x 3 steps x 32768 runs over the max-over-ranks time
+    assert abs(d["value"] * d["ms_per_step"] * 3 / 1e3 - 2 * 3 * 32768) < 1e-3 * 2 * 3 * 32768
+
+
+def test_single_rank_unchanged():
+    d = _bench("--gpus", "1", "--steps", "2", "--warmup", "0")
+    assert d["n_gpus"] == 1
+    assert "cpu_baseline" not in d

@@ -71,3 +71,18 @@ def test_gpu_sweep_run_multi_one_device_equals_sweep_run(msim):
     for x, y in zip(a, b):
         assert _rows(x.sums) == _rows(y.sums)
         assert x.stats_total == y.stats_total
+
+
+@pytest.mark.parametrize("preset", ["c2", "c3"])
+def test_gpu_run_sharded_side_stream_many_chunks(msim, preset):
+    """run_sharded on a non-current stream with several chunks reusing one output buffer: the adds and
+    the reduction are ordered after each chunk's kernels, so the sums equal one msim_run."""
+    import torch
+
+    from miningsimulation_amd.distributed import run_sharded
+
+    sim = msim.Simulation(msim.PRESETS[preset]())
+    n = 5000
+    st = torch.cuda.Stream()
+    got = run_sharded(sim, n, 1000, run_begin=123, stream=st, max_chunk=1024).cpu().tolist()
+    assert got == _rows(sim.run(n, 123, 1000, 0).sums)
