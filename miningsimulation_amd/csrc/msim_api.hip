@@ -146,15 +146,15 @@ int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables 
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
     std::lock_guard<std::mutex> g(c->mu);
-    const size_t pick_b = PICK_TAB * sizeof(PickEntry), log_b = LOG_TAB * sizeof(LogEntry);
+    const size_t pick_b = sizeof(PickTab), log_b = sizeof(LogTab);
     void *d = nullptr;
     for (const auto &t : c->tables)
         if (t.dev == dev && t.seg == seg && t.nseg >= nseg) d = t.ptr;
     if (!d) {
         const size_t jump_b = (size_t)nseg * 128 * 16;
         std::vector<char> h(pick_b + log_b + jump_b);
-        build_pick_table(c->perc, c->prop, c->self, (int)c->n, (PickEntry *)h.data());
-        build_log_table((LogEntry *)(h.data() + pick_b));
+        build_pick_table(c->perc, c->prop, c->self, (int)c->n, (PickTab *)h.data());
+        build_log_table((LogTab *)(h.data() + pick_b));
         build_jump_table(nseg, seg, (uint32_t *)(h.data() + pick_b + log_b));
         if (hipMalloc(&d, h.size()) != hipSuccess) return MSIM_E_HIP;
         if (hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -164,8 +164,8 @@ int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables 
         c->tables.push_back({dev, seg, nseg, d});
     }
     const char *b = (const char *)d;
-    out->pick = (const PickEntry *)b;
-    out->logt = (const LogEntry *)(b + pick_b);
+    out->pick = (const PickTab *)b;
+    out->logt = (const LogTab *)(b + pick_b);
     out->jump = (const uint32_t *)(b + pick_b + log_b);
     return MSIM_OK;
 }
@@ -192,7 +192,7 @@ void destroy_events(std::vector<hipEvent_t> &v)
 }
 
 // Process-wide log table (msim_fastdraw.h) per device, for msim_device_intervals.
-int global_log_table(const msim::LogEntry **out)
+int global_log_table(const msim::LogTab **out)
 {
     static std::mutex mu;
     static void *tab[MAX_DEVICES] = {nullptr};
@@ -200,17 +200,17 @@ int global_log_table(const msim::LogEntry **out)
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) return MSIM_E_HIP;
     std::lock_guard<std::mutex> g(mu);
     if (!tab[dev]) {
-        msim::LogEntry h[msim::LOG_TAB];
-        msim::build_log_table(h);
+        msim::LogTab h;
+        msim::build_log_table(&h);
         void *d = nullptr;
         if (hipMalloc(&d, sizeof(h)) != hipSuccess) return MSIM_E_HIP;
-        if (hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
+        if (hipMemcpy(d, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(d);
             return MSIM_E_HIP;
         }
         tab[dev] = d;
     }
-    *out = (const msim::LogEntry *)tab[dev];
+    *out = (const msim::LogTab *)tab[dev];
     return MSIM_OK;
 }
 
@@ -231,7 +231,7 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
     const WideGeom g = wide_geom(c->p.duration_ms);
     const size_t o_cf = 0, o_bkt = o_cf + 8 * ((size_t)m + 1), o_prop = (o_bkt + 2 * (size_t)WB_N + 7) / 8 * 8;
     const size_t o_log = o_prop + 8 * (size_t)m;
-    const size_t o_jm = (o_log + LOG_TAB * sizeof(LogEntry) + 255) / 256 * 256, o_jt = o_jm + 64 * 2048,
+    const size_t o_jm = (o_log + sizeof(LogTab) + 255) / 256 * 256, o_jt = o_jm + 64 * 2048,
                  o_js = o_jt + 64 * 2048, total = o_js + 2048;
     std::lock_guard<std::mutex> lk(c->mu);
     void *d = nullptr;
@@ -246,7 +246,7 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
         }
         build_wide_pick(c->wperc.data(), fthr.data(), m, (uint32_t)c->total_weight, (uint64_t *)(h.data() + o_cf),
                         (uint16_t *)(h.data() + o_bkt));
-        build_log_table((LogEntry *)(h.data() + o_log));
+        build_log_table((LogTab *)(h.data() + o_log));
         // jmain[l] = T^(l*S0); jtail[l] = T^(B0 + l*ST); jstep = T^(63*ST - 1)
         auto store = [](const Mat128 &mm, uint32_t *w) {
             for (int col = 0; col < 128; ++col) {
@@ -280,7 +280,7 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
     a->cf = (const uint64_t *)(b + o_cf);
     a->bucket = (const uint16_t *)(b + o_bkt);
     a->prop = (const int64_t *)(b + o_prop);
-    a->logt = (const LogEntry *)(b + o_log);
+    a->logt = (const LogTab *)(b + o_log);
     a->jmain = (const uint32_t *)(b + o_jm);
     a->jtail = (const uint32_t *)(b + o_jt);
     a->jstep = (const uint32_t *)(b + o_js);
@@ -558,7 +558,10 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
                 return rc == -3 ? MSIM_E_SELFISH : (rc == -2 ? MSIM_E_WEIGHTS : MSIM_E_INVALID);
             }
         }
-        c->pipe_ok = !sel && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
+        // the draw kernel's fast threshold holds delays below FTHR_CAP (262 s; msim_fastdraw.h)
+        bool prop_ok = true;
+        for (uint32_t k = 0; k < n; ++k) prop_ok = prop_ok && miners[k].propagation_ms < (int64_t)msim::FTHR_CAP;
+        c->pipe_ok = !sel && prop_ok && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
     } else {
         c->wide = true;
         c->pipe_ok = false;
@@ -768,7 +771,7 @@ int msim_device_log1p(const double *d_x, double *d_out, uint64_t n, void *stream
 int msim_device_intervals(const uint64_t *d_uniform, int64_t *d_out_ms, uint64_t n, void *stream)
 {
     if (!d_uniform || !d_out_ms) return MSIM_E_INVALID;
-    const msim::LogEntry *lt = nullptr;
+    const msim::LogTab *lt = nullptr;
     const int rc = global_log_table(&lt);
     if (rc) return rc;
     return msim::launch_intervals(lt, d_uniform, d_out_ms, n, (hipStream_t)stream) == hipSuccess ? MSIM_OK : MSIM_E_HIP;
@@ -1204,8 +1207,8 @@ int sample_impl(int mode, const msim_config *cfg, uint64_t seed, uint64_t n, int
         cf.assign(m + 1, 0);
         build_wide_pick(w.data(), fthr.data(), m, W, cf.data(), bucket.data());
     }
-    LogEntry lt[LOG_TAB];
-    build_log_table(lt);
+    LogTab lt;
+    build_log_table(&lt);
     const size_t bj = jumps.size() * 4, bc = cf.size() * 8, bb = bucket.size() * 2, bl = sizeof(lt), bo = nout * 8;
     char *d = nullptr;
     int rc = MSIM_OK;
@@ -1218,9 +1221,9 @@ int sample_impl(int mode, const msim_config *cfg, uint64_t seed, uint64_t n, int
     if (hipMemcpyAsync(pj, jumps.data(), bj, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pc, cf.data(), bc, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb, bucket.data(), bb, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(pl, lt, bl, hipMemcpyHostToDevice, st) != hipSuccess || hipMemsetAsync(po, 0, bo, st) != hipSuccess ||
+        hipMemcpyAsync(pl, &lt, bl, hipMemcpyHostToDevice, st) != hipSuccess || hipMemsetAsync(po, 0, bo, st) != hipSuccess ||
         launch_sample(mode, (const uint32_t *)pj, seed, n, S, (const uint64_t *)pc, (const uint16_t *)pb, m, W,
-                      0xFFFFFFFFFFFFFFFFull / W, (const LogEntry *)pl, (unsigned long long *)po, st) != hipSuccess ||
+                      0xFFFFFFFFFFFFFFFFull / W, (const LogTab *)pl, (unsigned long long *)po, st) != hipSuccess ||
         hipMemcpyAsync(host_out, po, bo, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
         rc = MSIM_E_HIP;
     (void)hipStreamDestroy(st);

@@ -19,6 +19,7 @@ namespace msim {
 
 __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
 
+
 // Both RNG states of the lane advanced by the same jump matrix (128 wave-uniform columns).
 __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rng &b)
 {
@@ -31,14 +32,15 @@ __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rn
         for (int i = 0; i < 32; ++i) {
             const uint4 c = cols[w * 32 + i];
             const uint32_t ma = 0u - ((sa[w] >> i) & 1u), mb = 0u - ((sb[w] >> i) & 1u);
-            oa0 ^= c.x & ma;
-            oa1 ^= c.y & ma;
-            oa2 ^= c.z & ma;
-            oa3 ^= c.w & ma;
-            ob0 ^= c.x & mb;
-            ob1 ^= c.y & mb;
-            ob2 ^= c.z & mb;
-            ob3 ^= c.w & mb;
+            // o ^= c & m as one v_bitop3_b32 (table of (src0 & src1) ^ src2: 0xF0 & 0xCC ^ 0xAA = 0x6A)
+            oa0 = __builtin_amdgcn_bitop3_b32(c.x, ma, oa0, 0x6A);
+            oa1 = __builtin_amdgcn_bitop3_b32(c.y, ma, oa1, 0x6A);
+            oa2 = __builtin_amdgcn_bitop3_b32(c.z, ma, oa2, 0x6A);
+            oa3 = __builtin_amdgcn_bitop3_b32(c.w, ma, oa3, 0x6A);
+            ob0 = __builtin_amdgcn_bitop3_b32(c.x, mb, ob0, 0x6A);
+            ob1 = __builtin_amdgcn_bitop3_b32(c.y, mb, ob1, 0x6A);
+            ob2 = __builtin_amdgcn_bitop3_b32(c.z, mb, ob2, 0x6A);
+            ob3 = __builtin_amdgcn_bitop3_b32(c.w, mb, ob3, 0x6A);
         }
     }
     a.s0 = (uint64_t)oa0 | ((uint64_t)oa1 << 32);
@@ -47,25 +49,32 @@ __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rn
     b.s1 = (uint64_t)ob2 | ((uint64_t)ob3 << 32);
 }
 
-// Side effects of one K1 lane (msim_pipeline.h draw_segment): LDS per-owner counters, wave-aggregated
-// appends to the dense episode list, the band's group records.
+// Side effects of one K1 lane (msim_pipeline.h draw_segment): LDS per-owner counters (one u32 per owner
+// and lane, [owner][lane]: conflict-free, and the increment is one ds_add_u32 of a constant), wave-
+// aggregated appends to the dense episode list, the band's group records.
+constexpr uint32_t K1_OWNERS = 2 * CNT_WORDS;  // 15 miners + PickFinder's fall-through (index 15)
+
 struct DevCtx {
     const DrawArgs &a;
     uint32_t (*cnt)[256];
+    uint64_t amask;  // active lanes of the wave (runs < n)
     uint32_t tid, lane, r, seg, jb, nsl;
-    bool active;
-    __device__ void count(uint32_t k) { atomicAdd(&cnt[k >> 1][tid], 1u << (16u * (k & 1u))); }
-    __device__ void slow(bool is_slow, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri,
-                         const Rng &rp)
+    // owner row k = info_finder(info) sits at byte offset k << 10 = info & (15 << INFO_K_SHIFT)
+    __device__ __forceinline__ void count(uint32_t info)
     {
-        const bool want = is_slow && active;
-        const uint64_t mask = __ballot(want);
-        if (!mask) return;  // wave-uniform
+        atomicAdd((uint32_t *)((char *)&cnt[0][tid] + (info & (15u << INFO_K_SHIFT))), 1u);
+    }
+    __device__ __forceinline__ bool vote(bool s) const { return (__builtin_amdgcn_ballot_w64(s) & amask) != 0ull; }
+    // the owner counters packed as the u16 pairs of the workspace layout (msim_pipeline.h CNT_WORDS)
+    __device__ __forceinline__ uint32_t packed(uint32_t w) const { return cnt[2 * w][tid] | (cnt[2 * w + 1][tid] << 16); }
+    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
+    {
+        const uint64_t mask = __builtin_amdgcn_ballot_w64(s) & amask;
         const int leader = __ffsll((unsigned long long)mask) - 1;
         uint32_t base = 0;
         if ((int)lane == leader) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
         base = __shfl(base, leader, 64);
-        if (!want) return;
+        if (!((mask >> lane) & 1ull)) return;
         const uint32_t idx =
             base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
         if (idx < a.lcap) {
@@ -93,7 +102,7 @@ struct DevCtx {
         gr.pad = 0;
         a.grec[gi * a.nr + r] = gr;
 #pragma unroll
-        for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = cnt[w][tid];
+        for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = packed(w);
     }
     __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * a.gps + g) * a.nr + r] = sum; }
 };
@@ -107,14 +116,18 @@ __global__ __launch_bounds__(256, MSIM_K1_WAVES) void msim_draws_kernel(const Dr
 __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
 #endif
 {
-    __shared__ LogEntry s_log[LOG_TAB];
-    __shared__ PickEntry s_pick[PICK_TAB];
-    __shared__ uint32_t s_cnt[CNT_WORDS][256];
+    // one LDS block: pick table, log table, owner counters
+    __shared__ struct {
+        PickTab pick;
+        LogTab log;
+        uint32_t cnt[K1_OWNERS][256];
+    } sm;
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = a.tab.logt[i];
-    for (uint32_t i = tid; i < PICK_TAB; i += 256) s_pick[i] = a.tab.pick[i];
+    for (uint32_t i = tid; i < sizeof(PickTab) / 4; i += 256) ((uint32_t *)&sm.pick)[i] = ((const uint32_t *)a.tab.pick)[i];
+    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&sm.log)[i] = ((const double *)a.tab.logt)[i];
+    auto s_cnt = sm.cnt;
 #pragma unroll
-    for (uint32_t w = 0; w < CNT_WORDS; ++w) s_cnt[w][tid] = 0;
+    for (uint32_t w = 0; w < K1_OWNERS; ++w) s_cnt[w][tid] = 0;
     __syncthreads();
 
     const uint32_t r = blockIdx.x * 256 + tid;  // slice-local run (< nr)
@@ -125,11 +138,11 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
 
     const uint32_t b0 = seg * a.seg;
-    DevCtx cx{a, s_cnt, tid, tid & 63u, r, seg, seg - a.band_lo, 0u, r < a.n};
-    const uint64_t tsum = draw_segment(cx, ri, rp, s_log, s_pick, b0, a.seg, seg >= a.band_lo);
+    DevCtx cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, tid & 63u, r, seg, seg - a.band_lo, 0u};
+    const uint64_t tsum = draw_segment(cx, ri, rp, &sm.log, &sm.pick, b0, a.seg, seg >= a.band_lo);
     a.segsum[(size_t)seg * a.nr + r] = tsum;
 #pragma unroll
-    for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = s_cnt[w][tid];
+    for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = cx.packed(w);
     a.nslow[(size_t)seg * a.nr + r] = cx.nsl;
 }
 
@@ -139,9 +152,9 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
 // compare: it is p1 = floor(100u / 2^64) or p1 + 1), or for weighted networks the finder itself.
 __global__ __launch_bounds__(256) void msim_word_draws_kernel(const WordArgs a)
 {
-    __shared__ LogEntry s_log[LOG_TAB];
+    __shared__ LogTab s_log;
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = a.logt[i];
+    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&s_log)[i] = ((const double *)a.logt)[i];
     __syncthreads();
     const uint32_t r = blockIdx.x * 256 + tid;  // slice-local run (< nr)
     const uint32_t seg = blockIdx.y;
@@ -160,7 +173,7 @@ __global__ __launch_bounds__(256) void msim_word_draws_kernel(const WordArgs a)
             uint32_t w[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t I = draw_interval(ri, s_log);
+                const uint32_t I = draw_interval(ri, &s_log);
                 const uint64_t u = rng_next(rp);
                 const uint64_t p1 = __umul64hi(u, W);
                 uint32_t code = (uint32_t)(u >= (p1 + 1) * mult ? p1 + 1 : p1);
@@ -189,7 +202,7 @@ hipError_t word_draws_blocks_per_cu(int *blocks)
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_word_draws_kernel, 256, 0);
 }
 
-__global__ void msim_interval_kernel(const LogEntry *__restrict__ lt, const uint64_t *__restrict__ u,
+__global__ void msim_interval_kernel(const LogTab *__restrict__ lt, const uint64_t *__restrict__ u,
                                      int64_t *__restrict__ out, uint64_t n)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -199,23 +212,23 @@ __global__ void msim_interval_kernel(const LogEntry *__restrict__ lt, const uint
     out[i] = ok ? q : interval_ms_exact_dev(u[i]);
 }
 
-__global__ void msim_pick_kernel(const PickEntry *__restrict__ pt, const uint64_t *__restrict__ u,
+__global__ void msim_pick_kernel(const PickTab *__restrict__ pt, const uint64_t *__restrict__ u,
                                  int32_t *__restrict__ out, uint64_t n)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t k = pick_info(u[i], pt) & 15u;
+    const uint32_t k = info_finder(pick_info(u[i], pt));
     out[i] = k == 15u ? -1 : (int32_t)k;
 }
 
-hipError_t launch_intervals(const LogEntry *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s)
+hipError_t launch_intervals(const LogTab *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(msim_interval_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lt, u, out, n);
     return hipGetLastError();
 }
 
-hipError_t launch_picks(const PickEntry *pt, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
+hipError_t launch_picks(const PickTab *pt, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s)
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(msim_pick_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pt, u, out, n);

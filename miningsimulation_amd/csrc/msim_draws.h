@@ -71,13 +71,35 @@ MSIM_HD uint64_t rotl64(uint64_t x, int k)
 #endif
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// One 64-bit add as ONE v_lshl_add_u64. Written as plain C++, LLVM reassociates `rot + s0` (rot built
+// from two alignbit halves) into two 64-bit adds plus a move; gfx950 issues every 64-bit integer op at
+// the rate of an alignbit (scripts/ubench/valu_rates.hip), so that costs a third of an RNG step.
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b)
+{
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+#endif
+
 MSIM_HD uint64_t rng_next(Rng &r)  // xoroshiro128++.h:26-34
 {
     const uint64_t s0 = r.s0;
     uint64_t s1 = r.s1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t result = add64(rotl64(s0 + s1, 17), s0);
+    s1 ^= s0;
+    // s0' = rotl(s0, 49) ^ s1 ^ (s1 << 21): one three-input XOR per half (v_bitop3_b32, table 0x96)
+    const uint64_t ro = rotl64(s0, 49), sh = s1 << 21;
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)ro, (uint32_t)s1, (uint32_t)sh, 0x96);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(ro >> 32), (uint32_t)(s1 >> 32), (uint32_t)(sh >> 32), 0x96);
+    r.s0 = ((uint64_t)hi << 32) | lo;
+#else
     const uint64_t result = rotl64(s0 + s1, 17) + s0;
     s1 ^= s0;
     r.s0 = rotl64(s0, 49) ^ s1 ^ (s1 << 21);
+#endif
     r.s1 = rotl64(s1, 28);
     return result;
 }

@@ -71,8 +71,8 @@ hipError_t launch_draws(const DrawArgs &a, hipStream_t s);
 hipError_t draws_blocks_per_cu(int *blocks);  // resident K1 workgroups per CU
 hipError_t launch_log1p(const double *x, double *out, uint64_t n, hipStream_t s);
 // Production draw paths of the pipeline (msim_fastdraw.h) over given uniforms (test/sampler surface).
-hipError_t launch_intervals(const LogEntry *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s);
-hipError_t launch_picks(const PickEntry *pt, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
+hipError_t launch_intervals(const LogTab *lt, const uint64_t *u, int64_t *out, uint64_t n, hipStream_t s);
+hipError_t launch_picks(const PickTab *pt, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
 constexpr int TPB = 256;  // 4 waves of 64 lanes per workgroup
 size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap);
 

@@ -67,8 +67,8 @@ struct PipeLayout {
 
 // Device tables (per config, per device): pick table, log table, jump matrices.
 struct PipeTables {
-    const PickEntry *pick;
-    const LogEntry *logt;
+    const PickTab *pick;
+    const LogTab *logt;
     const uint32_t *jump;  // nseg * 128 columns of 4 words
 };
 
@@ -188,11 +188,11 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
 __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u);
 #endif
 
-MSIM_HD uint32_t draw_interval(Rng &ri, const LogEntry *__restrict__ lt)
+MSIM_HD uint32_t draw_interval(Rng &ri, const LogTab *__restrict__ lt, FdConsts kc = MSIM_FD_DEFAULT)
 {
     const uint64_t u = rng_next(ri);
     bool ok;
-    const int32_t q = interval_ms_fast(u, lt, ok);
+    const int32_t q = interval_ms_fast(u, lt, ok, kc);
 #if defined(__HIP_DEVICE_COMPILE__)
     return (uint32_t)(ok ? q : interval_ms_exact_dev(u));
 #else
@@ -201,16 +201,16 @@ MSIM_HD uint32_t draw_interval(Rng &ri, const LogEntry *__restrict__ lt)
 }
 
 // Both draws of one block as a word: interval << 5 | finder (pick_info's low nibble).
-MSIM_HD uint32_t draw_word(Rng &ri, Rng &rp, const LogEntry *__restrict__ lt, const PickEntry *__restrict__ pt)
+MSIM_HD uint32_t draw_word(Rng &ri, Rng &rp, const LogTab *__restrict__ lt, const PickTab *__restrict__ pt)
 {
     const uint32_t I = draw_interval(ri, lt);
-    return (I << 5) | (pick_info(rng_next(rp), pt) & 15u);
+    return (I << 5) | info_finder(pick_info(rng_next(rp), pt));
 }
 
 // Episode draw source (K2): the stored words of its first two blocks, then the streams redrawn.
 struct EpSrc {
-    const LogEntry *lt;
-    const PickEntry *pt;
+    const LogTab *lt;
+    const PickTab *pt;
     Rng ri, rp;
     uint32_t nb, index, cur, nxt;
     bool have_nxt;
@@ -229,48 +229,91 @@ struct EpSrc {
     }
 };
 
+// The draws of four consecutive blocks, each by its fast path, with their exactness checks folded into
+// one flag; the rare quad that needs an exact path (an interval within 1 ns of a millisecond boundary,
+// or a PickFinder index the high word cannot settle: ~8e-6 of quads) is redrawn by draw_quad_exact from
+// the streams at its start. Batching four draws lets their table reads be in flight together.
+MSIM_HD bool draw_quad_fast(Rng &ri, Rng &rp, const LogTab *__restrict__ lt, const PickTab *__restrict__ pt,
+                            FdConsts kc, uint32_t (&I)[4], uint32_t (&info)[4])
+{
+    uint32_t ki = 0, kp = 0;  // largest acceptance keys of the quad
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t ui = rng_next(ri), up = rng_next(rp);
+        uint32_t a, b;
+        I[q] = (uint32_t)interval_ms_fast_key(ui, lt, a, kc);
+        info[q] = pt->info[pick_q_fast_key(up, b)];
+        ki = a > ki ? a : ki;
+        kp = b > kp ? b : kp;
+    }
+    return ki >= FD_OK_RANGE || kp >= PICK_RARE_LO;
+}
+MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, const PickTab *__restrict__ pt,
+                             uint32_t (&I)[4], uint32_t (&info)[4])
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        I[q] = draw_interval(ri, lt);  // the exact glibc sequence stays out of line (interval_ms_exact_dev)
+        info[q] = pt->info[pick_q_exact(rng_next(rp))];
+    }
+}
+
 // One (run, segment) worker: SEG blocks from the jumped RNG states. Ctx supplies the side effects:
-//   count(k)                          per-owner counter of this lane (+1 for owner k)
+//   count(info)                       per-owner counter of this lane (+1 for owner info_finder(info))
+//   vote(s)                           nonzero when s holds for some active lane of the wave (host: s)
 //   slow(s, block, offset, w0, w1, ri, rp)
-//                                     a non-fast block when s (offset = its find time minus the segment's
-//                                     start; its word, the next one and both streams after them)
+//                                     called after a nonzero vote: records a non-fast block when s
+//                                     (offset = its find time minus the segment's start; its word, the
+//                                     next one and both streams after them)
 //   group(g, sum)                     band only: sum of the group's intervals
 //   group_start(g, w0, ri, rp)        band only: before group g's first block (its word and the streams
 //                                     after it; snapshot the counters)
+// Blocks are drawn four at a time (draw_quad_fast); the streams after a block inside a quad, needed only
+// by the rare non-fast block, are re-stepped from the quad's start. Time is summed per group in 32 bits
+// (32 intervals < 2^25 ms each) and folded into 64 bits per group.
 template <class Ctx>
-MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogEntry *__restrict__ lt,
-                              const PickEntry *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
+MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restrict__ lt,
+                              const PickTab *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
 {
-    uint32_t Icur = draw_interval(ri, lt);
+    const FdConsts kc = fd_consts();
+    uint32_t Icur = draw_interval(ri, lt, kc);
     uint32_t infocur = pick_info(rng_next(rp), pt);
     uint64_t tsum = 0;
-    uint32_t gacc = 0;
-    for (uint32_t q4 = 0; q4 < seg / 4; ++q4) {
-        if (band && (q4 & 7u) == 0) cx.group_start(q4 >> 3, (Icur << 5) | (infocur & 15u), ri, rp);
+    for (uint32_t g = 0; g < seg / GROUP; ++g) {
+        if (band) cx.group_start(g, (Icur << 5) | info_finder(infocur), ri, rp);
+        uint32_t gacc = 0;
+        for (uint32_t q4 = 0; q4 < GROUP / 4; ++q4) {
+            const Rng ri0 = ri, rp0 = rp;  // after the quad's first "current" block
+            uint32_t I[4], info[4];
+            if (draw_quad_fast(ri, rp, lt, pt, kc, I, info)) draw_quad_exact(ri0, rp0, lt, pt, I, info);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t Inext = draw_interval(ri, lt);  // I_{i+1}
-            const uint32_t infonext = pick_info(rng_next(rp), pt);
-            tsum += Icur;
-            gacc += Icur;
-            const uint32_t k = infocur & 15u;
-            const bool fast = Inext > (infocur >> 4);
-            cx.count(k);
-            cx.slow(!fast, b0 + q4 * 4 + (uint32_t)q, tsum, (Icur << 5) | k, (Inext << 5) | (infonext & 15u), ri, rp);
-            Icur = Inext;
-            infocur = infonext;
+            for (int q = 0; q < 4; ++q) {
+                gacc += Icur;
+                const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
+                cx.count(infocur);
+                if (cx.vote(slow)) {
+                    Rng a = ri0, b = rp0;  // the streams after block i+1
+                    for (int t = 0; t <= q; ++t) {
+                        rng_next(a);
+                        rng_next(b);
+                    }
+                    cx.slow(slow, b0 + g * GROUP + q4 * 4 + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
+                            (I[q] << 5) | info_finder(info[q]), a, b);
+                }
+                Icur = I[q];
+                infocur = info[q];
+            }
         }
-        if (band && (q4 & 7u) == 7u) {
-            cx.group(q4 >> 3, gacc);
-            gacc = 0;
-        }
+        if (band) cx.group(g, gacc);
+        tsum += gacc;
     }
     return tsum;
 }
 
 // ---------------------------------------------------------------- K3 lane body (shared host/device)
+// Adds the M owner counters of a packed row; returns PickFinder's fall-through count (owner 15).
 template <int M>
-MSIM_HD void add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, size_t stride)
+MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, size_t stride)
 {
 #pragma unroll
     for (int w = 0; w < (M + 1) / 2; ++w) {
@@ -278,6 +321,7 @@ MSIM_HD void add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, size
         F[2 * w] += c & 0xFFFFu;
         if (2 * w + 1 < M) F[2 * w + 1] += c >> 16;
     }
+    return src[(size_t)(CNT_WORDS - 1) * stride] >> 16;
 }
 
 // Combine one run r of a slice. Returns false when the run must be recomputed by the retry path.
@@ -300,7 +344,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             break;
         }
         T += ss;
-        add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr);
+        if (add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr)) return false;  // fell through
     }
     if (e < (int)a.band_lo) return false;  // past the pre-generated draws or outside the band
     // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153).
@@ -315,7 +359,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         T += gs;
     }
     if (G == a.gps) return false;
-    add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr);
+    if (add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr)) return false;
     const uint32_t bg = (uint32_t)e * a.seg + G * GROUP;
     uint32_t n_end = 0, klast = 15u;
     int64_t t_last = 0;
@@ -335,6 +379,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             }
             T = Tn;
             klast = wd & 15u;
+            if (klast == 15u) return false;  // PickFinder fell through (simulation.h:220): the retry reports it
 #pragma unroll
             for (int kk = 0; kk < M; ++kk) F[kk] += (klast == (uint32_t)kk) ? 1u : 0u;
         }

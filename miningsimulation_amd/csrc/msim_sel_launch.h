@@ -52,7 +52,7 @@ struct SelParams {
 };
 
 struct WordArgs {
-    const LogEntry *logt;
+    const LogTab *logt;
     const uint32_t *jump;  // nseg * 128 columns of 4 words
     uint64_t run_begin;    // absolute index of the slice's first run
     uint32_t seed_base;

@@ -144,7 +144,7 @@ inline WideGeom wide_geom(int64_t duration_ms)
 // Draw source of one run from a candidate on: both streams, exact interval (draw_interval), wide pick.
 struct WideSrc {
     Rng ri, rp;
-    const LogEntry *lt;
+    const LogTab *lt;
     const uint64_t *cf;
     const uint16_t *bucket;
     uint32_t W;

@@ -65,7 +65,7 @@ struct W1Lds {
 };
 
 // Lane segment of nblk blocks starting at block b0 (RNG states positioned at draw b0).
-__device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogEntry *__restrict__ lt, Rng &ri, Rng &rp,
+__device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogTab *__restrict__ lt, Rng &ri, Rng &rp,
                                uint32_t nblk, uint32_t b0, uint32_t phase, uint32_t lane, uint32_t r, uint32_t &flast,
                                uint32_t &nc, uint32_t &pick_err_blk, uint32_t &err)
 {
@@ -118,7 +118,7 @@ __device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogEntry
 __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
 {
     extern __shared__ uint64_t sh64[];
-    __shared__ LogEntry s_log[LOG_TAB];
+    __shared__ LogTab s_log;
     __shared__ uint32_t s_cc[4];
     const uint32_t m = a.m, tid = threadIdx.x;
     uint64_t *s_cf = sh64;                                    // [m + 1]
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
     for (uint32_t i = tid; i <= m; i += 256) s_cf[i] = a.cf[i];
     for (uint32_t i = tid; i < WB_N; i += 256) s_bkt[i] = a.bucket[i];
     for (uint32_t i = tid; i < 4 * m; i += 256) s_hist[i] = 0;
-    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = a.logt[i];
+    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&s_log)[i] = ((const double *)a.logt)[i];
     if (tid < 4) s_cc[tid] = 0;
     __syncthreads();
 
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
         const Rng ris = ri, rps = rp;
         uint32_t nc = 0;
         flast = fprev;
-        const uint64_t tsum = w1_segment(a, s, s_log, ri, rp, nblk, b0, ph, lane, r, flast, nc, pick_err_blk, err);
+        const uint64_t tsum = w1_segment(a, s, &s_log, ri, rp, nblk, b0, ph, lane, r, flast, nc, pick_err_blk, err);
         const uint64_t excl = wave_excl_scan(tsum, lane);
         const uint64_t t0 = Tph + excl, tend = t0 + tsum;
         lanes[(size_t)ph * 64 + lane] = WideLane{t0, nc, 0u};
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
                 lf = Ls == 0 ? fprev : fprev_lane;
                 tl = t0;
                 for (uint32_t b = 0; b < nblk; ++b) {
-                    T += (uint32_t)draw_interval(i2, s_log);
+                    T += (uint32_t)draw_interval(i2, &s_log);
                     uint32_t th;
                     const uint32_t f = wide_pick(rng_next(p2), s.cf, s.bucket, a.W, a.mult, th);
                     if ((int64_t)T >= D) {
@@ -562,15 +562,15 @@ template <int MODE>
 __global__ __launch_bounds__(256) void msim_sample_kernel(const uint32_t *__restrict__ pow2_jumps, uint64_t seed,
                                                            uint64_t n, uint32_t S, const uint64_t *__restrict__ cf,
                                                            const uint16_t *__restrict__ bucket, uint32_t m, uint32_t W,
-                                                           uint64_t mult, const LogEntry *__restrict__ logt,
+                                                           uint64_t mult, const LogTab *__restrict__ logt,
                                                            unsigned long long *__restrict__ out)
 {
     extern __shared__ uint32_t s_hist[];  // MODE 0: [m + 1]
-    __shared__ LogEntry s_log[LOG_TAB];
+    __shared__ LogTab s_log;
     const uint32_t tid = threadIdx.x;
     if (MODE == 0)
         for (uint32_t i = tid; i <= m; i += 256) s_hist[i] = 0;
-    for (uint32_t i = tid; i < LOG_TAB; i += 256) s_log[i] = logt[i];
+    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&s_log)[i] = ((const double *)logt)[i];
     __syncthreads();
     const uint64_t j = (uint64_t)blockIdx.x * 256 + tid;
     const uint64_t b0 = j * S;
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(256) void msim_sample_kernel(const uint32_t *__rest
             const uint32_t k = wide_pick(rng_next(r), cf, bucket, W, mult, th);
             atomicAdd(&s_hist[k < m ? k : m], 1u);
         } else {
-            const uint64_t x = (uint64_t)draw_interval(r, s_log);
+            const uint64_t x = (uint64_t)draw_interval(r, &s_log);
             sum += x;
             sq += x * x;
             mx = x > mx ? x : mx;
@@ -607,7 +607,7 @@ __global__ __launch_bounds__(256) void msim_sample_kernel(const uint32_t *__rest
 
 // pow2_jumps: 32 matrices T^(S * 2^b) (msim_jump.h layout) in device memory.
 hipError_t launch_sample(int mode, const uint32_t *pow2_jumps, uint64_t seed, uint64_t n, uint32_t S, const uint64_t *cf,
-                         const uint16_t *bucket, uint32_t m, uint32_t W, uint64_t mult, const LogEntry *logt,
+                         const uint16_t *bucket, uint32_t m, uint32_t W, uint64_t mult, const LogTab *logt,
                          unsigned long long *out, hipStream_t s)
 {
     const uint64_t threads = (n + S - 1) / S;

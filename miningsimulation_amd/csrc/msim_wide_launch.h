@@ -14,7 +14,7 @@ struct WideArgs {
     const uint64_t *cf;       // [m + 1] cumulative weight | fast threshold << 32 (msim_wide.h wide_pick)
     const uint16_t *bucket;   // [WB_N]
     const int64_t *prop;                   // [m] propagation (ms)
-    const LogEntry *logt;
+    const LogTab *logt;
     const uint32_t *jmain;  // [64][128] uint4: T^(lane * S0)
     const uint32_t *jtail;  // [64][128] uint4: T^(B0 + lane * ST)
     const uint32_t *jstep;  // [128] uint4: T^(63 * ST - 1) (next tail chunk)
@@ -100,7 +100,7 @@ size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch);
 hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, const WideOut &out, hipStream_t s,
                        std::vector<hipEvent_t> *w1_events);
 hipError_t launch_sample(int mode, const uint32_t *pow2_jumps, uint64_t seed, uint64_t n, uint32_t S, const uint64_t *cf,
-                         const uint16_t *bucket, uint32_t m, uint32_t W, uint64_t mult, const LogEntry *logt,
+                         const uint16_t *bucket, uint32_t m, uint32_t W, uint64_t mult, const LogTab *logt,
                          unsigned long long *out, hipStream_t s);
 hipError_t launch_wide_picks(const WideArgs &a, const uint64_t *u, int32_t *out, uint64_t n, hipStream_t s);
 

@@ -9,10 +9,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <initializer_list>
+
 #include "../../miningsimulation_amd/csrc/msim_draws.h"
 #include "../../miningsimulation_amd/csrc/msim_fastdraw.h"
 
-static msim::LogEntry g_log[msim::LOG_TAB];
+static msim::LogTab g_log;
 
 static int64_t ref_interval(uint64_t u)
 {
@@ -30,7 +32,7 @@ struct Job {
 static void check_fast(uint64_t u, Job *j)
 {
     bool ok;
-    const int32_t q = msim::interval_ms_fast(u, g_log, ok);
+    const int32_t q = msim::interval_ms_fast(u, &g_log, ok);
     const int64_t fast = ok ? (int64_t)q : msim::interval_ms_of(u);
     if (!ok) j->fallbacks++;
     if (fast != ref_interval(u)) {
@@ -40,7 +42,7 @@ static void check_fast(uint64_t u, Job *j)
     // error of the approximation itself (before the margin test), in ns of 6e11*E + 0.5
     const double e = -log1p((double)(u >> 11) * -0x1.0p-53);
     const double yref = msim::BLOCK_INTERVAL_NS * e + 0.5;
-    const double err = fabs(msim::interval_fast_z(u, g_log) * 1e6 - yref);
+    const double err = fabs(msim::interval_fast_z(u, &g_log) * 1e6 - yref);
     if (err > j->max_err_ns) j->max_err_ns = err;
 }
 
@@ -78,9 +80,9 @@ static uint64_t check_picks(uint64_t seed)
             left -= (int)perc[k];
         }
         perc[m - 1] = (uint64_t)left;
-        for (int k = 0; k < m; ++k) prop[k] = (int64_t)(msim::rng_next(r) % 40000);
-        msim::PickEntry tab[msim::PICK_TAB];
-        msim::build_pick_table(perc, prop, self, m, tab);
+        for (int k = 0; k < m; ++k) prop[k] = (int64_t)(msim::rng_next(r) % 40000);  // < FTHR_CAP
+        msim::PickTab tab;
+        msim::build_pick_table(perc, prop, self, m, &tab);
         auto scan = [&](uint64_t u) {
             uint64_t i = 0;
             for (int k = 0; k < m; ++k) {
@@ -90,10 +92,13 @@ static uint64_t check_picks(uint64_t seed)
             return 15;
         };
         auto test = [&](uint64_t u) {
-            const uint32_t info = msim::pick_info(u, tab);
-            const int k = (int)(info & 15u);
-            const uint32_t fthr = info >> 4;
-            const uint32_t want_thr = k < 15 ? (uint32_t)prop[k] : msim::FTHR_NEVER;
+            const uint32_t info = msim::pick_info(u, &tab);
+            bool rare;
+            const uint32_t qf = msim::pick_q_fast(u, rare);
+            if (!rare && tab.info[qf] != info) bad++;  // the fast index is exact whenever it claims to be
+            const int k = (int)msim::info_finder(info);
+            const uint32_t fthr = msim::info_fthr(info);
+            const uint32_t want_thr = k < 15 ? (uint32_t)prop[k] : msim::FTHR_CAP;
             if (k != scan(u) || fthr != want_thr) bad++;
         };
         for (int i = 0; i < 20000; ++i) test(msim::rng_next(r));
@@ -104,6 +109,11 @@ static uint64_t check_picks(uint64_t seed)
         test(~0ull);
         test(~0ull - 15);
         test(~0ull - 16);
+        for (uint64_t c = 1; c <= 100; ++c) {  // u_hi just below the point where 100 u_hi / 2^32 reaches c
+            const uint64_t h = ((c << 32) + 99) / 100 - 1;
+            for (int64_t dh = -2; dh <= 0; ++dh)
+                for (uint64_t lo : {0ull, 1ull, 0x7FFFFFFFull, 0xFFFFFFF0ull, 0xFFFFFFFFull}) test(((h + dh) << 32) | lo);
+        }
     }
     return bad;
 }
@@ -142,7 +152,7 @@ int main(int argc, char **argv)
 {
     const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 10000000ull;
     const int th = argc > 2 ? atoi(argv[2]) : 8;
-    msim::build_log_table(g_log);
+    msim::build_log_table(&g_log);
     Job *jobs = (Job *)calloc((size_t)th, sizeof(Job));
     pthread_t *t = (pthread_t *)calloc((size_t)th, sizeof(pthread_t));
     for (int i = 0; i < th; ++i) {

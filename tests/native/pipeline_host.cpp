@@ -23,7 +23,12 @@ struct HostCtx {
     std::vector<uint32_t> *slots, *gsum, *gcum;
     std::vector<GroupRec> *grec;
     std::vector<EpEntry> *list;
-    void count(uint32_t k) { cnt[k >> 1] += 1u << (16u * (k & 1u)); }
+    void count(uint32_t info)
+    {
+        const uint32_t k = info_finder(info);
+        cnt[k >> 1] += 1u << (16u * (k & 1u));
+    }
+    bool vote(bool s) const { return s; }
     void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         if (!s) return;
@@ -49,11 +54,11 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     L.nr = n;  // no padding on the host
     if (cap_override) L.cap = cap_override;
     L.lcap = 0xFFFFFFF0u;
-    std::vector<PickEntry> pick(PICK_TAB);
-    std::vector<LogEntry> logt(LOG_TAB);
+    PickTab pick;
+    LogTab logt;
     std::vector<uint32_t> jump((size_t)L.nseg * 128 * 4);
-    build_pick_table(perc, prop, self, M, pick.data());
-    build_log_table(logt.data());
+    build_pick_table(perc, prop, self, M, &pick);
+    build_log_table(&logt);
     build_jump_table(L.nseg, L.seg, jump.data());
     std::vector<GroupRec> grec((size_t)L.nband * L.gps * n);
     std::vector<uint32_t> segcnt((size_t)L.nseg * CNT_WORDS * n), nslow((size_t)L.nseg * n),
@@ -90,7 +95,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
             cx.gsum = &gsum;
             cx.gcum = &gcum;
             cx.list = &list;
-            segsum[(size_t)j * n + r] = draw_segment(cx, ri, rp, logt.data(), pick.data(), j * L.seg, L.seg, j >= L.band_lo);
+            segsum[(size_t)j * n + r] = draw_segment(cx, ri, rp, &logt, &pick, j * L.seg, L.seg, j >= L.band_lo);
             for (uint32_t w = 0; w < CNT_WORDS; ++w) segcnt[((size_t)j * CNT_WORDS + w) * n + r] = cx.cnt[w];
             nslow[(size_t)j * n + r] = cx.nsl;
         }
@@ -107,7 +112,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     a.band_lo = L.band_lo;
     a.lcap = L.lcap;
     a.rec_words = L.rec_words;
-    a.tab = PipeTables{pick.data(), logt.data(), jump.data()};
+    a.tab = PipeTables{&pick, &logt, jump.data()};
     a.grec = grec.data();
     a.segsum = segsum.data();
     a.segcnt = segcnt.data();

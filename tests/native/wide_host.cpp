@@ -39,8 +39,8 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
     std::vector<uint32_t> fthr(m);
     for (uint32_t k = 0; k < m; ++k) fthr[k] = prop[k] < (int64_t)FTHR_NEVER ? (uint32_t)prop[k] : FTHR_NEVER;
     build_wide_pick(w, fthr.data(), m, (uint32_t)W, cf.data(), bucket.data());
-    std::vector<LogEntry> lt(LOG_TAB);
-    build_log_table(lt.data());
+    LogTab lt;
+    build_log_table(&lt);
     const uint64_t mult = 0xFFFFFFFFFFFFFFFFull / W;
     uint32_t neps = 0, n_retry = 0;
     for (uint32_t r = 0; r < n; ++r) {
@@ -52,7 +52,7 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
         int64_t t = 0;
         // draw until the first block at >= D, plus one more (its successor decides fast/slow)
         for (;;) {
-            const uint32_t x = draw_interval(ri, lt.data());
+            const uint32_t x = draw_interval(ri, &lt);
             uint32_t th;
             const uint32_t f = wide_pick(rng_next(rp), cf.data(), bucket.data(), (uint32_t)W, mult, th);
             t += x;
@@ -78,11 +78,11 @@ extern "C" int wide_host_run(const uint64_t *w, const int64_t *prop, uint32_t m,
         for (uint32_t s = 0; s < n_end && !err; ++s) {
             if (s < cursor) continue;
             if (!(I[s + 1] <= fthr[F[s]])) continue;  // fast block
-            WideSrc src{SI[s + 1], SP[s + 1], lt.data(), cf.data(), bucket.data(), (uint32_t)W, mult};
+            WideSrc src{SI[s + 1], SP[s + 1], &lt, cf.data(), bucket.data(), (uint32_t)W, mult};
             WideEpOut o;
             wide_episode<WE_FAST, WA_FAST>(prop, m, D, s, T[s], F[s], I[s + 1], F[s + 1], src, o);
             if (o.flags & WREC_RETRY) {  // the device's retry pass: same episode, larger capacities
-                WideSrc src2{SI[s + 1], SP[s + 1], lt.data(), cf.data(), bucket.data(), (uint32_t)W, mult};
+                WideSrc src2{SI[s + 1], SP[s + 1], &lt, cf.data(), bucket.data(), (uint32_t)W, mult};
                 wide_episode<WE, WA>(prop, m, D, s, T[s], F[s], I[s + 1], F[s + 1], src2, o);
                 ++n_retry;
             }
