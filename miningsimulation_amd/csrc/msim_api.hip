@@ -307,7 +307,18 @@ uint32_t word_draw_slots()
     return (uint32_t)(cus * blocks * 4);
 }
 
+// E1 draws in-lane by default (SelFastDraw), for a single network and for sweeps alike: on MI355X the
+// configs[3] grid (360 points x 8192 runs) ran 2.92 s in-lane vs 3.63 s reading D1's shared word stream
+// (profiles/r03/sweep_b_*.txt). MSIM_SEL_WORDS=1 restores the word stream (A/B measurements).
+bool sel_use_words(uint32_t np)
+{
+    (void)np;
+    if (const char *e = getenv("MSIM_SEL_WORDS")) return atoi(e) != 0;
+    return false;
+}
+
 struct SelWs {
+    bool words;
     msim::SelLayout L;
     uint32_t wpp, err_cap;
     size_t cold_lanes;
@@ -318,7 +329,15 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     SelWs w;
-    w.L = msim::sel_layout_for(duration_ms, rpp, SEL_SLICE_BUDGET, word_draw_slots());
+    w.words = sel_use_words(np);
+    if (w.words) {
+        w.L = msim::sel_layout_for(duration_ms, rpp, SEL_SLICE_BUDGET, word_draw_slots());
+    } else {  // one slice of every run (up to 2^22 runs: cold slots ~1.4 GiB), no words
+        w.L = msim::sel_layout_for(duration_ms, 256, SEL_SLICE_BUDGET, 1);
+        const uint64_t want = (rpp + 255) / 256 * 256;
+        w.L.nr = (uint32_t)(want < (1ull << 22) ? want : (1ull << 22));
+        w.L.words_bytes = 0;
+    }
     w.wpp = (uint32_t)((rpp + msim::TPB - 1) / msim::TPB);
     w.err_cap = (uint32_t)(rpp * np);  // every lane can be retried: the list never overflows
     const size_t nv = 6 * (size_t)m;
@@ -396,7 +415,8 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     a.seed_base = seed_base;
     a.nr = w.L.nr;
     a.nb = w.L.nb;
-    a.words = (const uint32_t *)(ws + w.words_off);
+    a.words = w.words ? (const uint32_t *)(ws + w.words_off) : nullptr;
+    a.logt = wt.logt;
     a.partials = (uint64_t *)(ws + w.partials_off);
     a.retry_sums = retry;
     a.records = (uint32_t *)d_per_run;
@@ -426,9 +446,11 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     for (uint64_t s0 = 0; s0 < rpp; s0 += w.L.nr) {
         const uint32_t sn = (uint32_t)((rpp - s0) < w.L.nr ? (rpp - s0) : w.L.nr);
         da.run_begin = run_begin + s0;
-        event(draw_events);
-        if (launch_word_draws(da, s) != hipSuccess) return MSIM_E_HIP;
-        event(draw_events);
+        if (w.words) {
+            event(draw_events);
+            if (launch_word_draws(da, s) != hipSuccess) return MSIM_E_HIP;
+            event(draw_events);
+        }
         a.s0 = (uint32_t)s0;
         a.sn = sn;
         event(engine_events);

@@ -145,46 +145,61 @@ struct SelWordSrc {
         pop();
         return true;
     }
+    __device__ __forceinline__ void spec() {}
+    __device__ __forceinline__ void fill() {}
 };
 
-// The reference's draws recomputed in-lane (retry): exact NextBlockInterval and PickFinder with
-// integer weights (q = floor(u / MULT) is p1 = floor(W u / 2^64) or p1 + 1; first k with cum_k > q).
-struct SelRngSrc {
+__device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
+
+// The reference's draws made in-lane (SelFifo drawers). PickFinder with integer weights: q = floor(u / MULT)
+// is p1 = floor(W u / 2^64) or p1 + 1, and the finder is the first k with cum_k > q (simulation.h:213-221).
+template <int M>
+__device__ __forceinline__ uint32_t sel_pick_weighted(uint64_t u, const SelParams *P)
+{
+    const uint64_t p1 = __umul64hi(u, (uint64_t)P->W);
+    const uint64_t q = u >= (p1 + 1) * P->mult ? p1 + 1 : p1;
+    uint32_t f = 0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) f += P->cum[j] <= q ? 1u : 0u;  // M = the network's miner count
+    return f;
+}
+
+// Exact sequence (E2 retries): glibc's log1p for every interval.
+template <int M>
+struct SelExactDraw {
     Rng ri, rp;
     const SelParams *P;
-    uint32_t hI, hk;  // a block drawn by peek() and not yet consumed
-    bool held;
-    __device__ bool next(uint32_t &I, uint32_t &k)
+    __device__ void draw(uint32_t &I, uint32_t &k)
     {
-        if (held) {
-            held = false;
-            I = hI;
-            k = hk;
-            return true;
-        }
         I = (uint32_t)next_interval(ri);
-        const uint64_t u = rng_next(rp);
-        const uint64_t p1 = __umul64hi(u, (uint64_t)P->W);
-        const uint64_t q = u >= (p1 + 1) * P->mult ? p1 + 1 : p1;
-        uint32_t f = 0;
-        for (uint32_t j = 0; j < P->m; ++j) f += P->cum[j] <= q ? 1u : 0u;
-        k = f;
-        return true;
+        k = sel_pick_weighted<M>(rng_next(rp), P);
     }
-    __device__ bool peek(uint32_t &I, uint32_t &k)
+};
+
+// Fast sequence (E1 without a word stream): K1's table interval with its exactness check and exact
+// fallback (msim_fastdraw.h), the finder through the LDS code table for percentages (W = 100) or the
+// weighted scan otherwise (wave-uniform choice).
+template <int M>
+struct SelFastDraw {
+    Rng ri, rp;
+    const LogTab *lt;     // LDS
+    const uint8_t *lut;   // LDS: finder of q = floor(u / PERC_MULTIPLIER)
+    const SelParams *P;
+    FdConsts kc;
+    bool wt;
+    __device__ __forceinline__ void draw(uint32_t &I, uint32_t &k)
     {
-        if (!held) {
-            next(hI, hk);
-            held = true;
+        I = draw_interval(ri, lt, kc);
+        const uint64_t u = rng_next(rp);
+        if (!wt) {
+            bool rare;
+            uint32_t q = pick_q_fast(u, rare);
+            if (rare) q = pick_q_exact(u);
+            k = lut[q];  // q = 100: PickFinder falls through (finder >= m)
+        } else {
+            k = sel_pick_weighted<M>(u, P);
         }
-        I = hI;
-        k = hk;
-        return true;
     }
-    __device__ void pop() { held = false; }
-    __device__ void pop_if(bool p) { held = held && !p; }
-    __device__ void prefetch() {}
-    __device__ void settle() {}
 };
 
 template <int M>
@@ -306,6 +321,7 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
                                 park(r);
                                 mode = 3;
                             } else {
+                                src.fill();  // the settled form starts every step with two held draws
 #if SEL_MC_LDS
                                 tb.save(mcs, TPB);
 #else
@@ -379,14 +395,40 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
     o.err = err;
 }
 
-// E1: one lane per (point, run of the slice); workgroups never straddle points.
-template <int M, int NS, int NA, int NG, int NQ, int NC>
+// E1: one lane per (point, run of the slice); workgroups never straddle points. FAST: the lane makes its
+// draws itself (SelFastDraw); otherwise it reads the slice's word stream written by D1 (sweeps).
+template <int M, int NS, int NA, int NG, int NQ, int NC, bool FAST, class Src>
+__device__ __forceinline__ void sel_lane(const SelArgs &a, const SelParams *P, Src &src, SelOut &o, uint32_t *s_cnt_lane,
+                                         const int64_t *s_prop, uint32_t *mcs, size_t lane)
+{
+    SelDevEnv<M> env{s_cnt_lane, s_prop, P->prop[0], P->uniform_prop != 0, a.cold + lane, a.cold_lanes};
+    const int64_t D = P->duration_ms;
+    if (a.force_retry) {
+        o.err = SERR_CAP;
+    } else if constexpr (NS == 1) {
+        sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, mcs);
+    } else {
+        Sel<M, NS, NA, NG, NQ, NC> s;
+        s.init(P->m, P->sids);
+        s.begin(src);
+        for (;;) {
+            src.prefetch();
+            const bool live = s.step(env, src, D);
+            src.settle();
+            if (!live) break;
+        }
+        s.finish(env, D, o);
+    }
+}
+
+template <int M, int NS, int NA, int NG, int NQ, int NC, bool FAST>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_sel_kernel(const SelArgs a)
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
     __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
     __shared__ int64_t s_prop[MAXM];
     __shared__ uint8_t s_lut[128];
+    __shared__ LogTab s_log[1];  // FAST only
     const uint32_t tid = threadIdx.x;
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
     const uint32_t point = a.plist[blockIdx.x / wps], blk = blockIdx.x % wps;
@@ -396,6 +438,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         uint32_t f = 0;
         for (int j = 0; j < MAXM; ++j) f += P->ccum[j] <= tid ? 1u : 0u;
         s_lut[tid] = (uint8_t)f;
+    }
+    if constexpr (FAST) {
+        if (tid < LOG_TAB) {
+            s_log[0].invc[tid] = a.logt->invc[tid];
+            s_log[0].A[tid] = a.logt->A[tid];
+        }
     }
 #pragma unroll
     for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
@@ -408,34 +456,29 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
     for (int i = 0; i < 6 * M; ++i) v[i] = 0;
     if (active) {
         const size_t lane = (size_t)(blockIdx.x / wps) * wps * TPB + (size_t)blk * TPB + tid;  // < cold_lanes
-        SelDevEnv<M> env{&s_cnt[0][tid], s_prop, P->prop[0], P->uniform_prop != 0, a.cold + lane, a.cold_lanes};
-        SelWordSrc<M> src;
-        src.p = reinterpret_cast<const uint4 *>(a.words) + (size_t)lr * (SEL_TILE / 4);
-        src.row = (size_t)a.nr * (SEL_TILE / 4);
-        src.nb = a.nb;
-#if SEL_LUT
-        src.lut = s_lut;
-#endif
-        src.init(P->ccum);
         SelOut o;
-        const int64_t D = P->duration_ms;
-        if (a.force_retry) {
-            o.err = SERR_CAP;
+        if constexpr (FAST) {
+            const uint64_t run = a.run_begin + rel;
+            SelFifo<SelFastDraw<M>> src;
+            src.d.ri = rng_seed(seed_interval(a.seed_base, run));
+            src.d.rp = rng_seed(seed_picker(a.seed_base, run));
+            src.d.lt = s_log;
+            src.d.lut = s_lut;
+            src.d.P = P;
+            src.d.kc = fd_consts();
+            src.d.wt = P->W != 100u;
+            src.n = 0;
+            sel_lane<M, NS, NA, NG, NQ, NC, FAST>(a, P, src, o, &s_cnt[0][tid], s_prop, &s_mc[0][tid], lane);
         } else {
-            if constexpr (NS == 1) {
-                sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid]);
-            } else {
-                Sel<M, NS, NA, NG, NQ, NC> s;
-                s.init(P->m, P->sids);
-                s.begin(src);
-                for (;;) {
-                    src.prefetch();
-                    const bool live = s.step(env, src, D);
-                    src.settle();
-                    if (!live) break;
-                }
-                s.finish(env, D, o);
-            }
+            SelWordSrc<M> src;
+            src.p = reinterpret_cast<const uint4 *>(a.words) + (size_t)lr * (SEL_TILE / 4);
+            src.row = (size_t)a.nr * (SEL_TILE / 4);
+            src.nb = a.nb;
+#if SEL_LUT
+            src.lut = s_lut;
+#endif
+            src.init(P->ccum);
+            sel_lane<M, NS, NA, NG, NQ, NC, FAST>(a, P, src, o, &s_cnt[0][tid], s_prop, &s_mc[0][tid], lane);
         }
         if (o.err) {
             const uint32_t pos = atomicAdd(a.counts, 1u);
@@ -472,7 +515,11 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
     const SelParams *P = a.pts + point;
     const uint64_t run = a.run_begin + rel;
     SelDevEnv<M> env{&s_cnt[0][tid], P->prop, P->prop[0], P->uniform_prop != 0, a.cold + idx, a.cold_lanes};
-    SelRngSrc src{rng_seed(seed_interval(a.seed_base, run)), rng_seed(seed_picker(a.seed_base, run)), P};
+    SelFifo<SelExactDraw<M>> src;
+    src.d.ri = rng_seed(seed_interval(a.seed_base, run));
+    src.d.rp = rng_seed(seed_picker(a.seed_base, run));
+    src.d.P = P;
+    src.n = 0;
     SelOut o;
     if constexpr (NS == 1) {  // the mixed schedule, with the engine's wide capacities
         sel_mixed<M, Sel<M, NS, 4, 16, 4, SEL_NC>>(env, src, P, P->duration_ms, o, &s_mc[0][tid]);
@@ -509,10 +556,14 @@ static hipError_t launch_sel_ns(const SelArgs &a, hipStream_t s)
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
     // one selfish miner: the mixed schedule, whose engine episodes are local (one hot slot of each kind
     // flags no run of the configs[3] grid, tests/test_sel_host.py)
-    if constexpr (NS == 1)
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-    else
-        hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+    const bool fast = a.words == nullptr;
+    if constexpr (NS == 1) {
+        if (fast) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, true>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, false>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+    } else {
+        if (fast) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC, true>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC, false>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -9,8 +9,10 @@
 //                               table; weighted networks store the finder itself (code < 16).
 //                               Layout: tiles of 32 words per run, [block / 32][run][32], so a worker's
 //                               stores and an engine lane's loads both stay inside 128-byte lines.
-//   E1 msim_sel_kernel          one lane per (point, run): the entity engine over the run's words;
-//                               per-run MinerStats terms reduced per workgroup (fixed-point integers).
+//   E1 msim_sel_kernel          one lane per (point, run): the settled form + entity engine over the run's
+//                               draws, made in-lane (a single network: no word stream) or read from D1's
+//                               words (a multi-point sweep); per-run MinerStats terms reduced per workgroup
+//                               (fixed-point integers).
 //   E2 msim_sel_retry_kernel    one lane per flagged run: the engine with wide capacities and the draws
 //                               recomputed in-lane from the seeds, atomically added to per-point sums.
 //   F  msim_sel_finalize        one workgroup per (point, summed value).
@@ -74,7 +76,8 @@ struct SelArgs {
     uint32_t seed_base;
     uint32_t s0, sn;        // slice: runs [s0, s0 + sn) of every point (s0 a multiple of TPB)
     uint32_t nr, nb;        // word geometry of the slice
-    const uint32_t *words;
+    const uint32_t *words;  // null: E1 draws in-lane (SelFastDraw) and D1 does not run
+    const LogTab *logt;     // interval table of the in-lane draws
     uint64_t *partials;     // [n_points][wpp][6M]
     uint64_t *retry_sums;   // [n_points][6M]
     uint32_t *records;      // [n_points * rpp][M][2] or null

@@ -34,19 +34,84 @@
 
 namespace msim {
 
+// A FIFO of up to three held draws in front of a drawer that makes the reference's draws in-lane
+// (void D::draw(uint32_t &interval_ms, uint32_t &finder)). In the settled form it holds two draws at the
+// start of every step and spec() adds the third from streams that advance whatever the step's outcome, so
+// the draw arithmetic has no dependency on the transition it runs beside; a lane that leaves the form
+// keeps all three for the engine, which takes them first (next/peek), then draws on demand.
+template <class D>
+struct SelFifo {
+    D d;
+    uint32_t I0, k0, I1, k1, I2, k2;
+    uint32_t n;  // held draws
+    MSIM_HD bool peek(uint32_t &I, uint32_t &k)
+    {
+        if (n == 0u) {
+            d.draw(I0, k0);
+            n = 1u;
+        }
+        I = I0;
+        k = k0;
+        return true;
+    }
+    MSIM_HD void pop()
+    {
+        I0 = I1;
+        k0 = k1;
+        I1 = I2;
+        k1 = k2;
+        n -= 1u;
+    }
+    MSIM_HD void pop_if(bool p)
+    {
+        I0 = p ? I1 : I0;
+        k0 = p ? k1 : k0;
+        I1 = p ? I2 : I1;
+        k1 = p ? k2 : k1;
+        n -= p ? 1u : 0u;
+    }
+    MSIM_HD bool next(uint32_t &I, uint32_t &k)
+    {
+        peek(I, k);
+        pop();
+        return true;
+    }
+    MSIM_HD void spec()  // settled form: n == 2 here (fill() on every entry into the form)
+    {
+        d.draw(I2, k2);
+        n = 3u;
+    }
+    MSIM_HD void fill()
+    {
+        if (n == 0u) {
+            d.draw(I0, k0);
+            n = 1u;
+        }
+        if (n == 1u) {
+            d.draw(I1, k1);
+            n = 2u;
+        }
+    }
+    MSIM_HD void prefetch() {}
+    MSIM_HD void settle() {}
+};
+
 template <int M>
 struct SelMacro {
-    static constexpr int NPW = (M + 1) / 2;
+    // The honest branch's composition and the honest stale blocks not yet flushed are kept per HONEST slot
+    // (miner j's slot is j minus 1 if j is above the selfish miner), 16 bits per slot, four slots per
+    // 64-bit word: one shift and one 64-bit add per find, one add per resolution.
+    static constexpr int NP = M > 1 ? (M + 2) / 4 : 1;
     int64_t T;             // time of the pending find
     uint32_t k;            // its finder
     uint32_t F, h, w;      // settled state (see above)
-    uint32_t pend[NPW];    // honest branch: blocks per honest miner, 16 bits each
-    uint32_t stp[NPW];     // honest stale blocks not yet flushed to C_S, same packing
+    uint64_t pend[NP];     // honest branch: blocks per honest slot
+    uint64_t stp[NP];      // honest stale blocks not yet flushed to C_S, same packing
     uint32_t sst;          // selfish stale blocks not yet flushed
     uint32_t Ff;           // F at the last flush (stale added since <= F - Ff keeps stp's fields < 2^16)
 
     // The state as NW words at p[0], p[stride], ... (a lane's LDS column while the wave runs engine steps).
-    static constexpr int NW = 8 + 2 * NPW;
+    static constexpr int NW = 8 + 4 * NP;
     MSIM_HD void save(uint32_t *p, int stride) const
     {
         p[0] = (uint32_t)T;
@@ -58,9 +123,11 @@ struct SelMacro {
         p[6 * stride] = sst;
         p[7 * stride] = Ff;
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) {
-            p[(8 + i) * stride] = pend[i];
-            p[(8 + NPW + i) * stride] = stp[i];
+        for (int i = 0; i < NP; ++i) {
+            p[(8 + 2 * i) * stride] = (uint32_t)pend[i];
+            p[(9 + 2 * i) * stride] = (uint32_t)(pend[i] >> 32);
+            p[(8 + 2 * NP + 2 * i) * stride] = (uint32_t)stp[i];
+            p[(9 + 2 * NP + 2 * i) * stride] = (uint32_t)(stp[i] >> 32);
         }
     }
     MSIM_HD void load(const uint32_t *p, int stride)
@@ -73,13 +140,27 @@ struct SelMacro {
         sst = p[6 * stride];
         Ff = p[7 * stride];
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) {
-            pend[i] = p[(8 + i) * stride];
-            stp[i] = p[(8 + NPW + i) * stride];
+        for (int i = 0; i < NP; ++i) {
+            pend[i] = ((uint64_t)p[(9 + 2 * i) * stride] << 32) | p[(8 + 2 * i) * stride];
+            stp[i] = ((uint64_t)p[(9 + 2 * NP + 2 * i) * stride] << 32) | p[(8 + 2 * NP + 2 * i) * stride];
         }
     }
 
-    MSIM_HD uint32_t pend_of(int j) const { return (pend[j >> 1] >> (16 * (j & 1))) & 0xFFFFu; }
+    MSIM_HD static uint32_t slot(uint32_t j, uint32_t sid) { return j - (j > sid ? 1u : 0u); }
+    MSIM_HD static uint32_t field(const uint64_t (&a)[NP], uint32_t s)
+    {
+        uint64_t v = 0;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) v = (s >> 2) == (uint32_t)i ? a[i] : v;
+        return (uint32_t)(v >> (16 * (s & 3u))) & 0xFFFFu;
+    }
+    MSIM_HD static void field_add(uint64_t (&a)[NP], uint32_t s, uint32_t v)
+    {
+        const uint64_t x = (uint64_t)v << (16 * (s & 3u));
+#pragma unroll
+        for (int i = 0; i < NP; ++i) a[i] += (s >> 2) == (uint32_t)i ? x : 0ull;
+    }
+    MSIM_HD uint32_t pend_of(uint32_t j, uint32_t sid) const { return field(pend, slot(j, sid)); }
 
     // Start of a run (main.cpp:138, 149): the first find, at the first interval; genesis is the prefix.
     template <class Src>
@@ -91,19 +172,22 @@ struct SelMacro {
         sst = 0;
         Ff = 0;
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) pend[i] = stp[i] = 0;
+        for (int i = 0; i < NP; ++i) pend[i] = stp[i] = 0;
         uint32_t I = 0;
         if (!src.peek(I, k)) return false;
         src.pop();
         T = (int64_t)I;
+        src.fill();
         return true;
     }
 
     // One find. Returns 0 (next find pending), 1 (this find needs the entity engine), 2 (run over: the
-    // next find is at or after D).
+    // next find is at or after D). src.spec() lets a source that draws in-lane produce a later draw that
+    // does not depend on this step's outcome, so its arithmetic overlaps the transition below.
     template <class Env, class Src>
     MSIM_HD int step(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
     {
+        src.spec();
         uint32_t I = 0, kn = 0;
         const bool have = src.peek(I, kn);
         const bool is_s = k == sid;
@@ -120,17 +204,15 @@ struct SelMacro {
         const bool tie = hon & !res & !swin;  // one more tied block each
         const bool rs = res | swin;
         // k's block joins the honest branch (a resolving branch is cleared below)
-        const uint32_t inc = hon ? 1u << (16 * (k & 1u)) : 0u;
+        field_add(pend, slot(k, sid), hon ? 1u : 0u);
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) pend[i] += (k >> 1) == (uint32_t)i ? inc : 0u;
-#pragma unroll
-        for (int i = 0; i < NPW; ++i) stp[i] += swin ? pend[i] : 0u;
+        for (int i = 0; i < NP; ++i) stp[i] += swin ? pend[i] : 0ull;
         sst += res ? h : 0u;
         F += res ? h + 1u : (swin ? h + 2u : 0u);
         h = rs ? 0u : h + (tie ? 1u : 0u);
         w = sf ? w + 1u : (rs ? 0u : w - (tie ? 1u : 0u));
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) pend[i] = rs ? 0u : pend[i];
+        for (int i = 0; i < NP; ++i) pend[i] = rs ? 0ull : pend[i];
         env.add(C_F, k < (uint32_t)M ? k : 0u, ok ? 1u : 0u);
         src.pop_if(ok);
         T += ok ? (int64_t)I : 0;
@@ -143,14 +225,14 @@ struct SelMacro {
     {
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            const uint32_t v = (stp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            const uint32_t v = (uint32_t)j == sid ? 0u : field(stp, slot((uint32_t)j, sid));
             if (v) {
                 env.add(C_S, (uint32_t)j, v);
                 env.add(C_F, (uint32_t)j, 0u - v);
             }
         }
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) stp[i] = 0;
+        for (int i = 0; i < NP; ++i) stp[i] = 0;
         Ff = F;
         if (sst) {
             env.add(C_S, sid, sst);
@@ -187,7 +269,7 @@ struct SelMacro {
         s.init(m, sids);
 #pragma unroll
         for (int j = 0; j < M; ++j) {
-            const uint32_t p = pend_of(j);
+            const uint32_t p = (uint32_t)j == sid ? 0u : pend_of((uint32_t)j, sid);
             if (p) {
                 env.add(C_F, (uint32_t)j, 0u - p);
                 env.set(C_A, (uint32_t)j, p);
@@ -257,12 +339,12 @@ struct SelMacro {
         // convert: the common part joins the settled counters, the fork's blocks and the withheld ones are
         // counted provisionally, the honest branch's composition goes to pend[]
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) pend[i] = 0;
+        for (int i = 0; i < NP; ++i) pend[i] = 0;
         if (split) {
             const int pa = P.br ? C_B : C_A;
             for (int j = 0; j < M; ++j) {
                 const uint32_t cp = env.get(pa, (uint32_t)j);
-                pend[j >> 1] += cp << (16 * (j & 1));
+                if ((uint32_t)j != sid) field_add(pend, slot((uint32_t)j, sid), cp);
                 env.add(C_F, (uint32_t)j, cp);
                 env.set(C_A, (uint32_t)j, 0u);
                 env.set(C_B, (uint32_t)j, 0u);
@@ -271,7 +353,7 @@ struct SelMacro {
         for (int j = 0; j <= P.rt; ++j) {
             const uint32_t o = (uint32_t)(P.s >> (4 * j)) & 15u;
             env.add(C_F, o, 1u);
-            if (j >= d) pend[o >> 1] += 1u << (16 * (o & 1u));
+            if (j >= d) field_add(pend, slot(o, sid), 1u);
         }
         const uint32_t wn = (uint32_t)s.w[0];
         if (wn + hh) env.add(C_F, sid, wn + hh);
@@ -281,7 +363,7 @@ struct SelMacro {
         sst = 0;
         Ff = F;
 #pragma unroll
-        for (int i = 0; i < NPW; ++i) stp[i] = 0;
+        for (int i = 0; i < NP; ++i) stp[i] = 0;
         T = s.nbt_;
         k = s.kn_;
         return true;

@@ -29,34 +29,15 @@ struct HostEnv {
     bool fold_vote(bool due) { return due || (fold_every && ++nev % fold_every == 0); }
 };
 
-// Draws exactly as the reference's loop makes them (simulation.h:205-221), through the same packed
-// word the device draw kernel writes: interval << 7 | q, q = floor(u / MULT), finder = first k with
-// cum_k > q (weights summing to W; W = 100 is PickFinder with PERC_MULTIPLIER).
-struct HostSrc {
+// Draws exactly as the reference's loop makes them (simulation.h:205-221): finder = first k with
+// cum_k > q, q = floor(u / MULT) (weights summing to W; W = 100 is PickFinder with PERC_MULTIPLIER),
+// behind the device's draw FIFO (msim_selm.h SelFifo), so the held-draw bookkeeping of the in-lane path
+// is exercised too.
+struct HostDraw {
     Rng ri, rp;
     const uint64_t *cum;  // cumulative weights
     int m;
     uint64_t W, mult;
-    uint32_t hI = 0, hk = 0;  // drawn by peek(), not yet consumed
-    bool held = false;
-    bool peek(uint32_t &I, uint32_t &k)
-    {
-        if (!held) {
-            draw(hI, hk);
-            held = true;
-        }
-        I = hI;
-        k = hk;
-        return true;
-    }
-    void pop() { held = false; }
-    void pop_if(bool p) { held = held && !p; }
-    bool next(uint32_t &I, uint32_t &k)
-    {
-        peek(I, k);
-        pop();
-        return true;
-    }
     void draw(uint32_t &I, uint32_t &k)
     {
         I = (uint32_t)next_interval(ri);
@@ -67,6 +48,7 @@ struct HostSrc {
         k = f;  // == m: fell through (simulation.h:220)
     }
 };
+using HostSrc = SelFifo<HostDraw>;
 
 template <int M, int NS, int NA, int NG, int NQ, int NC>
 void run_one(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
@@ -133,6 +115,7 @@ void run_mixed(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t 
                     mc.finish(env, sid, o);
                     return;
                 }
+                src.fill();
                 macro = true;
             }
         }
@@ -198,12 +181,13 @@ extern "C" int sel_run(const uint64_t *weights, const int64_t *prop, const uint8
     }
     if (c != W) return -2;
     HostSrc src;
-    src.ri = rng_seed(seed_i);
-    src.rp = rng_seed(seed_p);
-    src.cum = cum;
-    src.m = m;
-    src.W = W;
-    src.mult = 0xFFFFFFFFFFFFFFFFull / W;
+    src.d.ri = rng_seed(seed_i);
+    src.d.rp = rng_seed(seed_p);
+    src.d.cum = cum;
+    src.d.m = m;
+    src.d.W = W;
+    src.d.mult = 0xFFFFFFFFFFFFFFFFull / W;
+    src.n = 0;
     SelOut o;
     memset(&o, 0, sizeof(o));
 #define CASE(MM)                                                                                 \
