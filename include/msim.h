@@ -31,14 +31,17 @@ extern "C" {
 #define MSIM_OK 0
 #define MSIM_E_INVALID (-1)  /* bad argument (null pointer, n == 0, negative duration/propagation) */
 #define MSIM_E_WEIGHTS (-2)  /* weights do not add up to 100 (or total_weight): the reference asserts */
-#define MSIM_E_SELFISH (-3)  /* more than 4 selfish miners, or a selfish miner in a network of > 15 miners */
+#define MSIM_E_SELFISH (-3)  /* reserved (round 2 rejected selfish networks the entity engine cannot serve;
+                                every network with selfish miners now runs, those on the general engine) */
 #define MSIM_E_MINERS (-4)   /* too many miners (see MSIM_MAX_*_MINERS), or duplicate miner ids */
 #define MSIM_E_HIP (-5)      /* HIP runtime error (no device, launch failure, out of memory) */
-#define MSIM_E_CAPACITY (-6) /* a run exceeded the compact state's capacity even on the retry kernel */
+#define MSIM_E_CAPACITY (-6) /* a run outgrew every window of the general engine (its last window holds every
+                                block a run of the config's duration can have: practically never) */
 #define MSIM_E_PICK (-7)     /* PickFinder fell through (simulation.h:220 assert): percentages < 100 */
 
-#define MSIM_MAX_MINERS 15        /* networks with a selfish miner (compact per-lane state) */
-#define MSIM_MAX_SELFISH 4        /* selfish miners per network (entity engine, msim_sel.h) */
+#define MSIM_MAX_MINERS 15        /* networks on the compact per-lane / entity-engine state */
+#define MSIM_MAX_SELFISH 4        /* selfish miners per network on the entity engine (msim_sel.h); more run on
+                                     the general engine (msim_general.h) */
 #define MSIM_MAX_WIDE_MINERS 4096 /* honest networks (large-network pipeline, BASELINE configs[4]) */
 
 typedef struct msim_miner {
@@ -79,8 +82,11 @@ int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms
  * total_weight W < 2^31, and PickFinder uses UINT64_MAX / W in place of PERC_MULTIPLIER
  * (simulation.h:18, 217). W = 100 is exactly msim_config_create. Honest networks of more than
  * MSIM_MAX_MINERS miners (up to MSIM_MAX_WIDE_MINERS), or with W != 100, run on the large-network
- * pipeline; networks with selfish miners (up to MSIM_MAX_SELFISH of them, any W) need
- * n <= MSIM_MAX_MINERS and run on the entity engine. */
+ * pipeline; networks with up to MSIM_MAX_SELFISH selfish miners and n <= MSIM_MAX_MINERS (any W) run
+ * on the entity engine; every other network with selfish miners (more selfish miners, or more miners) runs
+ * on the general engine (msim_general.h: the reference's explicit chains in bounded windows of device
+ * memory, slower per block, exact), which also finishes the runs the entity engine cannot (a selfish
+ * majority whose withheld chain outgrows its window). */
 int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
                                 msim_config **out);
 /* 1 when the config runs on the large-network pipeline (set MSIM_FORCE_WIDE=1 in the environment before
@@ -169,7 +175,9 @@ int msim_timing_read_stages(double *draws_ms, double *engine_ms, double *launch_
 /* How msim_launch will execute n_runs of this config on the current device. */
 typedef struct msim_pipeline_layout {
     uint32_t uses_pipeline;   /* 1: event-skipping pipeline (honest network); 2: large-network pipeline;
-                                 3: entity engine (selfish miners); 0: per-lane kernel */
+                                 3: entity engine (selfish miners); 4: general engine (slice_runs = its
+                                 lanes, segment_blocks = its first window, segments = window tiers,
+                                 blocks_per_run = its last window); 0: per-lane kernel */
     uint32_t slice_runs;      /* runs per pipeline slice */
     uint32_t segment_blocks;  /* blocks per draw-kernel worker */
     uint32_t segments;        /* workers per run */

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/msim.h"
+#include "msim_general_launch.h"
 #include "msim_jump.h"
 #include "msim_kernels.h"
 #include "msim_sel_launch.h"
@@ -22,6 +23,15 @@
 namespace {
 constexpr int MAX_DEVICES = 64;
 }
+
+// A network as the general engine reads it (msim_general.h): integer weights summing to W.
+struct GenHost {
+    int64_t duration_ms = 0;
+    uint64_t W = 100;
+    std::vector<uint64_t> w;
+    std::vector<int64_t> prop;
+    std::vector<uint8_t> self;
+};
 
 struct msim_config {
     msim::SimParams p;
@@ -50,6 +60,13 @@ struct msim_config {
     bool sel = false;
     msim::SelParams sp;
     std::vector<std::pair<int, void *>> stables;  // per device: SelParams + point list {0}
+    // Every network, as the general engine reads it: G finishes the runs the entity engine cannot, and
+    // serves alone (`general`) the networks no fast engine covers: selfish miners in networks of more than
+    // MSIM_MAX_MINERS miners, more than SEL_MAXS selfish miners, large honest networks whose fork rate the
+    // wide combine cannot hold.
+    GenHost gh;
+    bool general = false;
+    std::vector<std::pair<int, void *>> gtables;  // per device: GenParams + arrays
 };
 
 // A parameter sweep (BASELINE configs[3]): the points' parameter blocks, uploaded per device on first use.
@@ -71,6 +88,10 @@ struct msim_sweep {
     std::vector<Group> groups;
     std::vector<std::pair<int, void *>> sdev;  // (device, SelParams[n_points] + point lists)
     const msim_config *tab_cfg = nullptr;      // config whose log / jump tables the draws use
+    // General-engine view of every point (G finishes what E2 cannot; a sweep with a general point runs on G)
+    bool general = false;
+    std::vector<GenHost> gens;
+    std::vector<std::pair<int, void *>> gdev;  // (device, GenParams[n_points] + arrays)
 };
 
 namespace {
@@ -322,8 +343,14 @@ struct SelWs {
     msim::SelLayout L;
     uint32_t wpp, err_cap;
     size_t cold_lanes;
-    size_t counts_off, partials_off, retry_off, list_off, cold_off, words_off, total;
+    size_t counts_off, partials_off, retry_off, list_off, cold_off, words_off, gen_off, total;
+    msim::GenWs g;  // G, for the runs E2 cannot finish
 };
+
+// Workspace of the general engine: 512 MiB of windows when it only finishes other engines' runs, 2 GiB
+// when it serves a whole network (msim_general_launch.h gen_tiers).
+constexpr double GEN_FALLBACK_BUDGET = 512.0 * (1 << 20);
+constexpr double GEN_BUDGET = 2048.0 * (1 << 20);
 
 SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
 {
@@ -351,7 +378,9 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
     w.cold_lanes = e1 > w.err_cap ? e1 : (size_t)w.err_cap;
     w.cold_off = al(w.list_off + (size_t)w.err_cap * 4);
     w.words_off = al(w.cold_off + w.cold_lanes * msim::SEL_NC * sizeof(msim::ColdAct));
-    w.total = al(w.words_off + w.L.words_bytes);
+    w.gen_off = al(w.words_off + w.L.words_bytes);
+    w.g = msim::gen_ws_layout(m, duration_ms, w.err_cap, GEN_FALLBACK_BUDGET);
+    w.total = al(w.gen_off + w.g.total);
     return w;
 }
 
@@ -396,7 +425,8 @@ struct SelGroupDev {
 };
 
 // The slice loop of one launch: D1 (words) -> E1 per group -> E2 (retries) -> F.
-int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const std::vector<SelGroupDev> &groups,
+int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const msim::GenParams *d_gpts,
+                    const std::vector<SelGroupDev> &groups,
                     const msim::WordArgs &wt, const SelWs &w, char *ws, uint64_t run_begin, uint64_t rpp,
                     uint32_t seed_base, void *d_sums, void *d_per_run, void *d_best_height, void *d_status, hipStream_t s,
                     std::vector<hipEvent_t> *draw_events, std::vector<hipEvent_t> *engine_events)
@@ -404,9 +434,11 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     using namespace msim;
     uint32_t *counts = (uint32_t *)(ws + w.counts_off);
     uint64_t *retry = (uint64_t *)(ws + w.retry_off);
-    if (hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess ||
+    if (hipMemsetAsync(counts, 0, msim::GEN_C_WORDS * sizeof(uint32_t), s) != hipSuccess ||
         hipMemsetAsync(retry, 0, (size_t)np * 6 * m * 8, s) != hipSuccess)
         return MSIM_E_HIP;
+    char *gws = ws + w.gen_off;
+    uint32_t *gen_first = (uint32_t *)(gws + w.g.lists_off) + 2 * (size_t)w.g.list_cap;
     SelArgs a;
     a.pts = d_pts;
     a.rpp = (uint32_t)rpp;
@@ -427,6 +459,8 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     a.force_retry = getenv("MSIM_SEL_FORCE_RETRY") != nullptr ? 1u : 0u;
     a.cold = (ColdAct *)(ws + w.cold_off);
     a.cold_lanes = w.cold_lanes;
+    a.gen_list = gen_first;
+    a.force_gen = getenv("MSIM_SEL_FORCE_GEN") != nullptr ? 1u : 0u;
     WordArgs da = wt;
     da.seed_base = seed_base;
     da.nr = w.L.nr;
@@ -465,8 +499,124 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     a.s0 = 0;
     a.sn = 0;
     if (launch_sel_retry(a, m, max_ns, s) != hipSuccess) return MSIM_E_HIP;
+    GenArgs ga;
+    memset(&ga, 0, sizeof(ga));
+    ga.pts = d_gpts;
+    ga.rpp = (uint32_t)rpp;
+    ga.max_m = m;
+    ga.run_begin = run_begin;
+    ga.seed_base = seed_base;
+    ga.sums = retry;
+    ga.records = (uint32_t *)d_per_run;
+    ga.best_h = (uint32_t *)d_best_height;
+    ga.counts = counts;
+    if (launch_gen_tiers(ga, w.g, gws, gen_first, counts + GEN_C_L1, 0, s) != hipSuccess) return MSIM_E_HIP;
     if (launch_sel_finalize(a.partials, np, w.wpp, 6 * m, retry, (uint64_t *)d_sums, counts, (uint32_t *)d_status, s) !=
         hipSuccess)
+        return MSIM_E_HIP;
+    return MSIM_OK;
+}
+
+// Device GenParams of a list of networks (one per point) and their weight / delay / selfish arrays, in one
+// allocation whose pointers are device addresses.
+int gen_tables_upload(const std::vector<const GenHost *> &hs, void **out)
+{
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t np = hs.size();
+    size_t off = al(np * sizeof(msim::GenParams));
+    std::vector<size_t> o(np);
+    for (size_t i = 0; i < np; ++i) {
+        o[i] = off;
+        off = al(off + hs[i]->w.size() * 17);
+    }
+    std::vector<char> h(off, 0);
+    void *d = nullptr;
+    if (hipMalloc(&d, off) != hipSuccess) return MSIM_E_HIP;
+    for (size_t i = 0; i < np; ++i) {
+        const GenHost &g = *hs[i];
+        const size_t m = g.w.size();
+        uint64_t *cum = (uint64_t *)(h.data() + o[i]);
+        int64_t *prop = (int64_t *)(h.data() + o[i] + 8 * m);
+        uint8_t *self = (uint8_t *)(h.data() + o[i] + 16 * m);
+        uint64_t c = 0;
+        for (size_t k = 0; k < m; ++k) {
+            cum[k] = (c += g.w[k]);
+            prop[k] = g.prop[k];
+            self[k] = g.self[k];
+        }
+        msim::GenParams *gp = (msim::GenParams *)h.data() + i;
+        gp->duration_ms = g.duration_ms;
+        gp->mult = 0xFFFFFFFFFFFFFFFFull / g.W;
+        gp->m = (uint32_t)m;
+        gp->cum = (const uint64_t *)((char *)d + o[i]);
+        gp->prop = (const int64_t *)((char *)d + o[i] + 8 * m);
+        gp->self = (const uint8_t *)((char *)d + o[i] + 16 * m);
+    }
+    if (hipMemcpy(d, h.data(), off, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return MSIM_E_HIP;
+    }
+    *out = d;
+    return MSIM_OK;
+}
+
+// The per-device copy of a table list (lazily uploaded, cached under `mu`).
+int gen_cached(std::mutex &mu, std::vector<std::pair<int, void *>> &cache, const std::vector<const GenHost *> &hs,
+               const msim::GenParams **out)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return MSIM_E_HIP;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto &t : cache)
+        if (t.first == dev) {
+            *out = (const msim::GenParams *)t.second;
+            return MSIM_OK;
+        }
+    void *d = nullptr;
+    const int rc = gen_tables_upload(hs, &d);
+    if (rc) return rc;
+    cache.push_back({dev, d});
+    *out = (const msim::GenParams *)d;
+    return MSIM_OK;
+}
+
+// Workspace of a launch served by the general engine alone: counters, then G's lists and windows.
+struct GenOnlyWs {
+    msim::GenWs g;
+    size_t gen_off, total;
+};
+GenOnlyWs gen_only_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
+{
+    GenOnlyWs w;
+    w.g = msim::gen_ws_layout(m, duration_ms, (uint32_t)(rpp * np), GEN_BUDGET);
+    w.gen_off = 256;
+    w.total = w.gen_off + w.g.total;
+    return w;
+}
+
+// Every run of every point on G: codes point * rpp + rel, tier 1 over the whole range.
+int gen_launch_impl(uint32_t m, uint32_t np, const msim::GenParams *d_gpts, const GenOnlyWs &w, char *ws,
+                    uint64_t run_begin, uint64_t rpp, uint32_t seed_base, void *d_sums, void *d_per_run,
+                    void *d_best_height, void *d_status, hipStream_t s)
+{
+    using namespace msim;
+    uint32_t *counts = (uint32_t *)ws;
+    if (hipMemsetAsync(counts, 0, GEN_C_WORDS * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(d_sums, 0, (size_t)np * 6 * m * 8, s) != hipSuccess)
+        return MSIM_E_HIP;
+    GenArgs ga;
+    memset(&ga, 0, sizeof(ga));
+    ga.pts = d_gpts;
+    ga.rpp = (uint32_t)rpp;
+    ga.max_m = m;
+    ga.run_begin = run_begin;
+    ga.seed_base = seed_base;
+    ga.sums = (uint64_t *)d_sums;
+    ga.records = (uint32_t *)d_per_run;
+    ga.best_h = (uint32_t *)d_best_height;
+    ga.counts = counts;
+    if (launch_gen_tiers(ga, w.g, ws + w.gen_off, nullptr, nullptr, (uint32_t)(rpp * np), s) != hipSuccess ||
+        launch_gen_status(counts, (uint32_t *)d_status, s) != hipSuccess)
         return MSIM_E_HIP;
     return MSIM_OK;
 }
@@ -539,15 +689,26 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     if (total != total_weight) return MSIM_E_WEIGHTS;
     // Selfish miners run on the entity engine (msim_sel.h): up to SEL_MAXS of them, in networks of up to
     // MSIM_MAX_MINERS miners with any integer weights. The large-network path is honest-only.
-    if (nself > (uint32_t)msim::SEL_MAXS) return MSIM_E_SELFISH;
-    if (nself && n > MSIM_MAX_MINERS) return MSIM_E_SELFISH;
-    const bool sel = nself > 0;
+    // The entity engine takes up to SEL_MAXS selfish miners in networks of up to MSIM_MAX_MINERS miners; any
+    // other network with selfish miners runs on the general engine (msim_general.h), as does any network when
+    // MSIM_FORCE_GENERAL is set (test switch).
+    const bool gen = nself > (uint32_t)msim::SEL_MAXS || (nself && n > MSIM_MAX_MINERS) ||
+                     getenv("MSIM_FORCE_GENERAL") != nullptr;
+    const bool sel = nself > 0 && !gen;
     const bool narrow = n <= MSIM_MAX_MINERS && (total_weight == 100 || sel);
     const bool force_wide = getenv("MSIM_FORCE_WIDE") != nullptr && nself == 0;
     msim_config *c = new (std::nothrow) msim_config();
     if (!c) return MSIM_E_INVALID;
     c->n = n;
     c->total_weight = total_weight;
+    c->general = gen;
+    c->gh.duration_ms = duration_ms;
+    c->gh.W = total_weight;
+    for (uint32_t k = 0; k < n; ++k) {
+        c->gh.w.push_back(miners[k].perc);
+        c->gh.prop.push_back(miners[k].propagation_ms);
+        c->gh.self.push_back(miners[k].is_selfish ? 1 : 0);
+    }
     c->p.duration_ms = duration_ms;
     c->p.m = (int32_t)n;
     c->p.selfish = -1;
@@ -573,6 +734,8 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
                 c->p.prop[k] = k < (int)n ? miners[k].propagation_ms : 0;
                 c->p.thresh[k] = ~0ull;
             }
+        } else if (gen) {
+            c->p.m = (int32_t)n;
         } else {
             const int rc = msim::make_params(c->perc, c->prop, c->self, (int)n, duration_ms, &c->p);
             if (rc) {
@@ -583,7 +746,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         // the draw kernel's fast threshold holds delays below FTHR_CAP (262 s; msim_fastdraw.h)
         bool prop_ok = true;
         for (uint32_t k = 0; k < n; ++k) prop_ok = prop_ok && miners[k].propagation_ms < (int64_t)msim::FTHR_CAP;
-        c->pipe_ok = !sel && prop_ok && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
+        c->pipe_ok = !sel && !gen && prop_ok && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
     } else {
         c->wide = true;
         c->pipe_ok = false;
@@ -596,10 +759,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
             c->wprop[k] = miners[k].propagation_ms;
         }
         const msim::WideLayout L = wide_layout(c, 1);
-        if (msim::wide_w3_lds(n, L.rcap, L.g.nch) > 160 * 1024) {  // fork rate too high for the wide combine
-            delete c;
-            return MSIM_E_CAPACITY;
-        }
+        if (msim::wide_w3_lds(n, L.rcap, L.g.nch) > 160 * 1024) c->general = true;  // fork rate too high for W3
     }
     *out = c;
     return MSIM_OK;
@@ -660,6 +820,7 @@ void msim_config_destroy(msim_config *cfg)
     for (const auto &t : cfg->tables) (void)hipFree(t.ptr);
     for (const auto &t : cfg->wtables) (void)hipFree(t.second);
     for (const auto &t : cfg->stables) (void)hipFree(t.second);
+    for (const auto &t : cfg->gtables) (void)hipFree(t.second);
     delete cfg;
 }
 
@@ -668,6 +829,7 @@ uint32_t msim_config_miner_count(const msim_config *cfg) { return cfg ? cfg->n :
 size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
 {
     if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
+    if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total;
     if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
     if (cfg->sel) return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total;
     size_t t = ws_layout(cfg->n, n_runs).total;
@@ -680,6 +842,32 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
                 void *stream)
 {
     if (!cfg || !d_sums || !d_status || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    if (cfg->general) {
+        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
+        if (workspace_bytes < w.total) return MSIM_E_INVALID;
+        msim_config *c = const_cast<msim_config *>(cfg);
+        const msim::GenParams *gp = nullptr;
+        int rc = gen_cached(c->mu, c->gtables, {&cfg->gh}, &gp);
+        if (rc) return rc;
+        Timing &tm = timing();
+        std::unique_lock<std::mutex> lk(tm.mu);
+        hipEvent_t lb = nullptr, le = nullptr;
+        hipStream_t s = (hipStream_t)stream;
+        if (tm.on) {
+            if (hipEventCreate(&lb) == hipSuccess && hipEventCreate(&le) == hipSuccess) {
+                tm.launch.push_back(lb);
+                tm.launch.push_back(le);
+                (void)hipEventRecord(lb, s);
+            }
+            tm.launches++;
+        } else {
+            lk.unlock();
+        }
+        rc = gen_launch_impl(cfg->n, 1, gp, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums, d_per_run,
+                             d_best_height, d_status, s);
+        if (le) (void)hipEventRecord(le, s);
+        return rc;
+    }
     if (cfg->wide) {
         Timing &tm = timing();
         std::unique_lock<std::mutex> lk(tm.mu);
@@ -709,6 +897,9 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         const uint32_t *plist = nullptr;
         int rc = sel_config_tables(c, &pts, &plist);
         if (rc) return rc;
+        const msim::GenParams *gp = nullptr;
+        rc = gen_cached(c->mu, c->gtables, {&cfg->gh}, &gp);
+        if (rc) return rc;
         msim::WordArgs da;
         rc = sel_word_args(c, cfg->sp, w, &da);
         if (rc) return rc;
@@ -728,7 +919,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         } else {
             lk.unlock();
         }
-        rc = sel_launch_impl(cfg->n, 1, pts, groups, da, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
+        rc = sel_launch_impl(cfg->n, 1, pts, gp, groups, da, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
                              d_per_run, d_best_height, d_status, s, on ? &tm.k1 : nullptr, on ? &tm.engine : nullptr);
         if (le) (void)hipEventRecord(le, s);
         return rc;
@@ -916,17 +1107,25 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
     if (!w) return MSIM_E_INVALID;
     w->m = cfgs[0] ? cfgs[0]->n : 0;
     w->self = false;
+    bool any_general = false;
+    for (uint32_t i = 0; i < n_points; ++i) any_general = any_general || (cfgs[i] && cfgs[i]->general);
     for (uint32_t i = 0; i < n_points; ++i) {
-        // one miner count per sweep; narrow networks with percentages (the words are shared by all points)
-        if (!cfgs[i] || cfgs[i]->n != w->m || cfgs[i]->wide || cfgs[i]->total_weight != 100) {
+        // one miner count per sweep; narrow networks with percentages unless the sweep runs on the general
+        // engine (the per-lane and entity-engine sweeps share draws and tables between points)
+        if (!cfgs[i] || cfgs[i]->n != w->m || (!any_general && (cfgs[i]->wide || cfgs[i]->total_weight != 100))) {
             delete w;
             return MSIM_E_INVALID;
         }
         w->pts.push_back(cfgs[i]->p);
         w->self = w->self || cfgs[i]->p.selfish >= 0;
         w->sel = w->sel || cfgs[i]->sel;
+        w->general = w->general || cfgs[i]->general;
+        w->gens.push_back(cfgs[i]->gh);
+        w->max_duration = cfgs[i]->p.duration_ms > w->max_duration ? cfgs[i]->p.duration_ms : w->max_duration;
     }
-    if (w->sel) {
+    if (w->general) {  // a point only the general engine serves: every point on G
+        w->sel = false;
+    } else if (w->sel) {
         // every point on the entity engine; points grouped by selfish class
         for (uint32_t i = 0; i < n_points; ++i) {
             const msim_config *c = cfgs[i];
@@ -960,6 +1159,7 @@ void msim_sweep_destroy(msim_sweep *sw)
     if (!sw) return;
     for (const auto &d : sw->dev) (void)hipFree(d.second);
     for (const auto &d : sw->sdev) (void)hipFree(d.second);
+    for (const auto &d : sw->gdev) (void)hipFree(d.second);
     delete sw;
 }
 
@@ -969,6 +1169,7 @@ uint32_t msim_sweep_miner_count(const msim_sweep *sw) { return sw ? sw->m : 0u; 
 size_t msim_sweep_workspace_bytes(const msim_sweep *sw, uint64_t runs_per_point)
 {
     if (!sw || runs_per_point == 0 || runs_per_point * sw->pts.size() > MAX_LAUNCH_RUNS) return 0;
+    if (sw->general) return gen_only_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration).total;
     if (sw->sel) return sel_ws_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration).total;
     return sweep_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point).total;
 }
@@ -980,6 +1181,20 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
     if (!sw || !d_sums || !d_status || !d_workspace || runs_per_point == 0) return MSIM_E_INVALID;
     const uint32_t np = (uint32_t)sw->pts.size();
     if (runs_per_point * np > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
+    const msim::GenParams *gp = nullptr;
+    if (sw->general || sw->sel) {
+        msim_sweep *sm = const_cast<msim_sweep *>(sw);
+        std::vector<const GenHost *> hs;
+        for (const auto &g : sm->gens) hs.push_back(&g);
+        const int rc = gen_cached(sm->mu, sm->gdev, hs, &gp);
+        if (rc) return rc;
+        if (sw->general) {
+            const GenOnlyWs w = gen_only_layout(sw->m, np, runs_per_point, sw->max_duration);
+            if (workspace_bytes < w.total) return MSIM_E_INVALID;
+            return gen_launch_impl(sw->m, np, gp, w, (char *)d_workspace, run_begin, runs_per_point, seed_base, d_sums,
+                                   d_per_run, d_best_height, d_status, (hipStream_t)stream);
+        }
+    }
     if (sw->sel) {
         const SelWs w = sel_ws_layout(sw->m, np, runs_per_point, sw->max_duration);
         if (workspace_bytes < w.total) return MSIM_E_INVALID;
@@ -1015,7 +1230,7 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
         msim::WordArgs da;
         int rc = sel_word_args(const_cast<msim_config *>(sw->tab_cfg), sm->sps[0], w, &da);
         if (rc) return rc;
-        return sel_launch_impl(sw->m, np, (const msim::SelParams *)d, groups, da, w, (char *)d_workspace, run_begin,
+        return sel_launch_impl(sw->m, np, (const msim::SelParams *)d, gp, groups, da, w, (char *)d_workspace, run_begin,
                                runs_per_point, seed_base, d_sums, d_per_run, d_best_height, d_status,
                                (hipStream_t)stream, nullptr, nullptr);
     }
@@ -1157,6 +1372,16 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     if (!cfg || !out || n_runs == 0) return MSIM_E_INVALID;
     memset(out, 0, sizeof(*out));
     out->rho = cfg->rho;
+    if (cfg->general) {
+        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
+        out->uses_pipeline = 4;
+        out->slice_runs = (uint32_t)w.g.tier[0].lanes;
+        out->segment_blocks = w.g.tier[0].cap;
+        out->segments = (uint32_t)w.g.nt;
+        out->blocks_per_run = w.g.tier[w.g.nt - 1].cap;
+        out->workspace_bytes = w.total;
+        return MSIM_OK;
+    }
     if (cfg->wide) {
         const msim::WideLayout L = wide_layout(cfg, n_runs);
         out->uses_pipeline = 2;

@@ -85,6 +85,9 @@ MSIM_HD double u32_to_f64(uint32_t x) { return (double)x; }
 // a fresh register pair before every draw.
 // The leading coefficient (a multiplicand of the first step, beside the SGPR addend) lives in a VGPR:
 // one VOP3 instruction reads at most one SGPR on gfx950.
+#ifndef MSIM_FD_C5_VGPR
+#define MSIM_FD_C5_VGPR 1
+#endif
 struct FdConsts {
     double c1, c2, c3, c4, c5;
 };
@@ -96,7 +99,9 @@ MSIM_HD FdConsts fd_consts()
     asm("" : "+s"(k.c2));
     asm("" : "+s"(k.c3));
     asm("" : "+s"(k.c4));
+#if MSIM_FD_C5_VGPR
     asm("" : "+v"(k.c5));
+#endif
 #endif
     return k;
 }

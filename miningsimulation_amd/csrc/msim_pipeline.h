@@ -283,19 +283,25 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
         if (band) cx.group_start(g, (Icur << 5) | info_finder(infocur), ri, rp);
         uint32_t gacc = 0;
         for (uint32_t q4 = 0; q4 < GROUP / 4; ++q4) {
-            const Rng ri0 = ri, rp0 = rp;  // after the quad's first "current" block
             uint32_t I[4], info[4];
-            if (draw_quad_fast(ri, rp, lt, pt, kc, I, info)) draw_quad_exact(ri0, rp0, lt, pt, I, info);
+            if (draw_quad_fast(ri, rp, lt, pt, kc, I, info)) {
+                Rng a = ri, b = rp;  // back to the quad's start (no copy of it stays live)
+                for (int t = 0; t < 4; ++t) {
+                    rng_prev(a);
+                    rng_prev(b);
+                }
+                draw_quad_exact(a, b, lt, pt, I, info);
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 gacc += Icur;
                 const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
                 cx.count(infocur);
                 if (cx.vote(slow)) {
-                    Rng a = ri0, b = rp0;  // the streams after block i+1
-                    for (int t = 0; t <= q; ++t) {
-                        rng_next(a);
-                        rng_next(b);
+                    Rng a = ri, b = rp;  // the streams after block i+1: 3 - q steps back from the quad's end
+                    for (int t = q; t < 3; ++t) {
+                        rng_prev(a);
+                        rng_prev(b);
                     }
                     cx.slow(slow, b0 + g * GROUP + q4 * 4 + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
                             (I[q] << 5) | info_finder(info[q]), a, b);

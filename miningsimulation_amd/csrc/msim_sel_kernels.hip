@@ -2,6 +2,7 @@
 // per miner count (MSIM_M).
 #include <hip/hip_runtime.h>
 
+#include "msim_general_launch.h"
 #include "msim_kernels.h"
 #include "msim_reduce.h"
 #include "msim_sel_launch.h"
@@ -528,8 +529,14 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
         s.init(P->m, P->sids);
         s.run(env, src, P->duration_ms, o);
     }
-    if (o.err) {
-        atomicAdd(a.counts + 1, 1u);
+    if (o.err || a.force_gen) {  // G (msim_general.h) takes the run over: its windows have no such limits
+        if (a.gen_list) {
+            const uint32_t pos = atomicAdd(a.counts + GEN_C_L1, 1u);
+            if (pos < a.err_cap) a.gen_list[pos] = code;
+            else atomicAdd(a.counts + GEN_C_FAIL, 1u);
+        } else {
+            atomicAdd(a.counts + GEN_C_FAIL, 1u);
+        }
         return;
     }
     uint64_t v[6 * M];

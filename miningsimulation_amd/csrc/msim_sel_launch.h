@@ -15,6 +15,8 @@
 //                               (fixed-point integers).
 //   E2 msim_sel_retry_kernel    one lane per flagged run: the engine with wide capacities and the draws
 //                               recomputed in-lane from the seeds, atomically added to per-point sums.
+//   G  msim_gen_kernel          the runs E2 could not finish (a chain outgrew the 16-height window: a
+//                               selfish majority), on the general engine's explicit chains (msim_general.h).
 //   F  msim_sel_finalize        one workgroup per (point, summed value).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -88,6 +90,8 @@ struct SelArgs {
     uint32_t force_retry;   // test switch (MSIM_SEL_FORCE_RETRY): E1 flags every run, E2 computes all
     ColdAct *cold;          // cold slots: [SEL_NC][cold_lanes] (E1 lane = point-list slot * sn + run; E2 lane)
     size_t cold_lanes;
+    uint32_t *gen_list;     // runs E2 could not finish, for G (msim_general_launch.h), or null: counted as failed
+    uint32_t force_gen;     // test switch (MSIM_SEL_FORCE_GEN): E2 hands every run it gets to G
 };
 
 struct SelLayout {

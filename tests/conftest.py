@@ -36,9 +36,11 @@ def native_tests():
     chk = os.path.join(ROOT, "build", "draws_check")
     wide = os.path.join(ROOT, "build", "libwide_host.so")
     sel = os.path.join(ROOT, "build", "libsel_host.so")
-    if not all(os.path.exists(p) for p in (lib, chk, pipe, wide, sel)):
+    gen = os.path.join(ROOT, "build", "libgeneral_host.so")
+    if not all(os.path.exists(p) for p in (lib, chk, pipe, wide, sel, gen)):
         ge.build_native_tests()
-    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel}
+    return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel,
+            "general_host": gen}
 
 
 @pytest.fixture(scope="session")

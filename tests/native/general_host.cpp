@@ -1,0 +1,72 @@
+// general_host.cpp — TEST INFRASTRUCTURE: a host (CPU) build of the product's general engine
+// (miningsimulation_amd/csrc/msim_general.h) so its algorithm, including the window fold, can be checked
+// against the oracle without a GPU. Never part of the product path (libmsim.so is GPU-only).
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../miningsimulation_amd/csrc/msim_general.h"
+
+using namespace msim;
+
+namespace {
+
+struct HostStore {
+    uint32_t cap, m;
+    std::vector<uint32_t> o, sz, st, pr;
+    std::vector<int64_t> a;
+    HostStore(uint32_t m_, uint32_t cap_)
+        : cap(cap_), m(m_), o((size_t)m_ * cap_), sz(m_), st(m_), pr(m_), a((size_t)m_ * cap_)
+    {
+    }
+    uint32_t own(uint32_t k, uint32_t i) const { return o[(size_t)k * cap + i]; }
+    int64_t arr(uint32_t k, uint32_t i) const { return a[(size_t)k * cap + i]; }
+    void put(uint32_t k, uint32_t i, uint32_t ow, int64_t ar)
+    {
+        o[(size_t)k * cap + i] = ow;
+        a[(size_t)k * cap + i] = ar;
+    }
+    void set_arr(uint32_t k, uint32_t i, int64_t ar) { a[(size_t)k * cap + i] = ar; }
+    uint32_t size(uint32_t k) const { return sz[k]; }
+    void set_size(uint32_t k, uint32_t n) { sz[k] = n; }
+    void add_stale(uint32_t k) { ++st[k]; }
+    uint32_t stale(uint32_t k) const { return st[k]; }
+    void add_pre(uint32_t k, uint32_t v) { pr[k] += v; }
+    uint32_t pre(uint32_t k) const { return pr[k]; }
+};
+
+}  // namespace
+
+extern "C" {
+
+// One run with seeds (si, sp); weights sum to W. Returns the error bits (GERR_*); on success fills
+// found / stale [m] and the best chain height (length - 1).
+uint32_t gen_run(const uint64_t *weights, const int64_t *props, const uint8_t *selfish, int m, uint64_t W,
+                 int64_t duration, uint32_t si, uint32_t sp, uint32_t cap, uint32_t *found, uint32_t *stale,
+                 uint32_t *best_height, uint32_t *base)
+{
+    std::vector<uint64_t> cum(m);
+    uint64_t c = 0;
+    for (int k = 0; k < m; ++k) cum[k] = (c += weights[k]);
+    GenParams g;
+    memset(&g, 0, sizeof(g));
+    g.duration_ms = duration;
+    g.mult = 0xFFFFFFFFFFFFFFFFull / W;
+    g.m = (uint32_t)m;
+    g.cum = cum.data();
+    g.prop = props;
+    g.self = selfish;
+    HostStore s((uint32_t)m, cap);
+    Gen<HostStore> e(s, g);
+    GenOut o;
+    if (!e.run(rng_seed(si), rng_seed(sp), o)) return o.err;
+    for (int k = 0; k < m; ++k) {
+        found[k] = e.found((uint32_t)k, o);
+        stale[k] = s.stale((uint32_t)k);
+    }
+    *best_height = Gen<HostStore>::best_height(o);
+    *base = o.base;
+    return 0;
+}
+}

@@ -45,9 +45,7 @@ def test_config_validation_without_gpu(msim_lib_path):
     bad = [
         ([Miner(0, 60, 1000), Miner(1, 30, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 90
         ([Miner(0, 60, 1000), Miner(1, 50, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 110
-        ([Miner(k, 20, 1000, True) for k in range(5)], _lib.MSIM_E_SELFISH),      # > MSIM_MAX_SELFISH
         ([Miner(0, 50, 1000), Miner(0, 50, 1000)], _lib.MSIM_E_MINERS),             # duplicate id
-        ([Miner(k, 7 if k < 10 else 5, 1000, k == 0) for k in range(16)], _lib.MSIM_E_SELFISH),  # wide: honest only
         ([Miner(k, 1 if k < 100 else 0, 1000) for k in range(4097)], _lib.MSIM_E_MINERS),
         ([Miner(0, 50, -1), Miner(1, 50, 1000)], _lib.MSIM_E_INVALID),
     ]
@@ -64,6 +62,12 @@ def test_config_validation_without_gpu(msim_lib_path):
                       ([Miner(0, 7, 1000, True), Miner(1, 3, 1000)], 10)):
         sim = Simulation(miners, total_weight=W)
         assert not sim.wide and sim.pipeline_info(1024)["uses_pipeline"] == 3
+    # every other network with selfish miners runs on the general engine (msim_general.h): more than
+    # MSIM_MAX_SELFISH selfish miners, or selfish miners in networks of more than 15 miners, any W
+    for miners, W in (([Miner(k, 20, 1000, True) for k in range(5)], 100),
+                      ([Miner(k, 7 if k < 10 else 5, 1000, k == 0) for k in range(16)], 100),
+                      ([Miner(k, 1, 1000, k == 0) for k in range(16)], 16)):
+        assert Simulation(miners, total_weight=W).pipeline_info(1024)["uses_pipeline"] == 4
     # the large-network path (msim_wide.h): more than 15 honest miners, or integer weights
     assert Simulation([Miner(k, 7 if k < 10 else 5, 1000) for k in range(16)]).wide
     assert not Simulation(setup_miners()).wide
@@ -72,7 +76,6 @@ def test_config_validation_without_gpu(msim_lib_path):
     for miners, W, code in (
         (c5, 102401, _lib.MSIM_E_WEIGHTS),                                      # weights sum to 102400
         ([Miner(0, 1 << 31, 1000)], 1 << 31, _lib.MSIM_E_WEIGHTS),              # W >= 2^31
-        ([Miner(k, 1, 1000, k == 0) for k in range(16)], 16, _lib.MSIM_E_SELFISH),  # selfish: <= 15 miners
     ):
         try:
             Simulation(miners, total_weight=W)

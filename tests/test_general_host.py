@@ -1,0 +1,117 @@
+"""The product's general engine (miningsimulation_amd/csrc/msim_general.h), built for the host
+(tests/native/general_host.cpp, test-only), against the oracle: per-run found and stale counters and the
+best-chain height must be identical (bit-exact integer parity).
+
+The general engine serves what the fast engines cannot: selfish miners in networks of more
+than 15 miners, more than 4 selfish miners, and runs whose withheld chains outgrow the entity engine's
+window (a selfish majority). Its windows fold the common arrived prefix; small windows here force a fold
+every few blocks, so the fold is exercised far more often than on the device."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+DAY = 86_400_000
+GERR_CAP = 1
+
+
+@pytest.fixture(scope="module")
+def gen(native_tests):
+    lib = ctypes.CDLL(native_tests["general_host"])
+    lib.gen_run.restype = ctypes.c_uint32
+    lib.gen_run.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                            ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_uint64, ctypes.c_int64,
+                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                            ctypes.POINTER(ctypes.c_uint32)]
+
+    def run(weights, props, selfish, duration, si, sp, cap, W=100):
+        m = len(weights)
+        f = (ctypes.c_uint32 * m)()
+        s = (ctypes.c_uint32 * m)()
+        bh = ctypes.c_uint32()
+        base = ctypes.c_uint32()
+        err = lib.gen_run((ctypes.c_uint64 * m)(*weights), (ctypes.c_int64 * m)(*props),
+                          (ctypes.c_uint8 * m)(*[1 if x else 0 for x in selfish]), m, W, duration, si, sp, cap, f, s,
+                          ctypes.byref(bh), ctypes.byref(base))
+        return err, np.array([[f[k], s[k]] for k in range(m)], dtype=np.int64), bh.value, base.value
+
+    return run
+
+
+def _rand_weights(m, rng, total=100):
+    cuts = sorted(rng.sample(range(1, total), m - 1)) if m > 1 else []
+    b = [0] + cuts + [total]
+    return [b[i + 1] - b[i] for i in range(m)]
+
+
+def _check_batch(gen, oracle, weights, props, selfish, duration, n_runs, seed_base, cap, W=100, allow_cap=False):
+    """Runs 0..n-1 with the SURVEY seed convention (base + 2r, base + 2r + 1) vs the oracle's batch."""
+    f, s, _, _ = oracle.run_batch(weights, props, selfish, duration, n_runs, 0, seed_base, threads=8, total_weight=W)
+    folded = checked = 0
+    for r in range(n_runs):
+        si, sp = (seed_base + 2 * r) & 0xFFFFFFFF, (seed_base + 2 * r + 1) & 0xFFFFFFFF
+        err, res, bh, base = gen(weights, props, selfish, duration, si, sp, cap, W)
+        if err == GERR_CAP and allow_cap:
+            continue
+        assert err == 0, (err, weights, props, selfish, duration, r)
+        exp = np.stack([f[r], s[r]], axis=1)
+        assert np.array_equal(exp, res), (weights, props, selfish, duration, r, exp.tolist(), res.tolist())
+        assert bh == int(f[r].sum()), (bh, int(f[r].sum()))
+        folded += base > 0
+        checked += 1
+    return folded, checked
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_networks_any_selfish(gen, oracle, seed):
+    """1-15 miners, any number of selfish miners at any index, uniform or mixed delays (0 ms - 30 s)."""
+    rng = random.Random(7100 + seed)
+    folded = checked = 0
+    for _ in range(12):
+        m = rng.randint(1, 15)
+        w = _rand_weights(m, rng)
+        props = [rng.choice([0, 1, 100, 1000, 5000, 30000])] * m if rng.random() < 0.5 else \
+            [rng.choice([0, 2, 50, 700, 2000, 12000]) for _ in range(m)]
+        selfish = [rng.random() < 0.35 for _ in range(m)]
+        # small windows: a run whose selfish miners hold a majority may outgrow one (flagged, never wrong)
+        fo, ch = _check_batch(gen, oracle, w, props, selfish, rng.choice([DAY, 7 * DAY, 30 * DAY]), 4,
+                              rng.randrange(1 << 32), cap=rng.choice([48, 64, 256]), allow_cap=True)
+        folded += fo
+        checked += ch
+    assert folded > 8 and checked >= 24, (folded, checked)  # most runs checked, and the windows did fold
+
+
+def test_selfish_majority_two_miners(gen, oracle):
+    """Two selfish miners holding 70 % between them (the entity engine's window can overflow here)."""
+    _check_batch(gen, oracle, [35, 35, 20, 10], [1000] * 4, [True, True, False, False], 30 * DAY, 6, 4242,
+                 cap=4096)
+
+
+def test_selfish_single_majority(gen, oracle):
+    """One selfish miner with 60 %: its lead grows for the whole run, so the window must hold it."""
+    _check_batch(gen, oracle, [60, 25, 15], [100, 100, 100], [True, False, False], 30 * DAY, 4, 99, cap=8192)
+    # a window too small for that lead is flagged, never wrong
+    err, _, _, _ = gen([60, 25, 15], [100] * 3, [True, False, False], 30 * DAY, 99, 100, 64)
+    assert err == GERR_CAP
+
+
+def test_many_selfish(gen, oracle):
+    """Six selfish miners (the entity engine serves at most four)."""
+    _check_batch(gen, oracle, [10] * 6 + [20, 20], [1000] * 8, [True] * 6 + [False] * 2, 30 * DAY, 6, 7, cap=512)
+
+
+def test_large_network_one_selfish(gen, oracle):
+    """100 miners (integer weights summing to W = 1000) with one selfish miner at 30 %."""
+    rng = random.Random(5)
+    w = [300] + _rand_weights(99, rng, 700)
+    props = [1000] * 100
+    selfish = [True] + [False] * 99
+    _check_batch(gen, oracle, w, props, selfish, 7 * DAY, 3, 1000, cap=256, W=1000)
+
+
+def test_zero_duration_and_zero_delay(gen, oracle):
+    _check_batch(gen, oracle, [50, 30, 20], [0, 0, 0], [False, True, False], 0, 2, 3, cap=64)
+    _check_batch(gen, oracle, [50, 30, 20], [0, 0, 0], [False, True, False], 10 * DAY, 3, 3, cap=64)
+    _check_batch(gen, oracle, [100], [0], [True], 3 * DAY, 2, 11, cap=4096)

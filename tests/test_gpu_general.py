@@ -1,0 +1,118 @@
+"""The general engine G (msim_general.h, msim_general.hip) on the GPU, through the C ABI, against the oracle:
+per-run found and stale counters bit-exact.
+
+G serves every network with selfish miners that the entity engine does not (more than 4 selfish miners, a
+selfish miner in a network of more than 15 miners) and finishes the runs the entity engine cannot (a
+selfish majority whose withheld chain outgrows the 16-height window). These are exactly the networks
+round 2 rejected with MSIM_E_SELFISH / MSIM_E_CAPACITY (Missing #1-#2, Weak #10)."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DAY = 86_400_000
+D = 31_556_952_000
+
+
+@pytest.fixture(scope="module")
+def msim(msim_lib_path):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.cuda.set_device(0)
+    import miningsimulation_amd as m
+
+    return m
+
+
+def _rand_weights(m, rng, total=100):
+    cuts = sorted(rng.sample(range(1, total), m - 1)) if m > 1 else []
+    b = [0] + cuts + [total]
+    return [b[i + 1] - b[i] for i in range(m)]
+
+
+def _vs_oracle(msim, oracle, p, q, s, n, seed, dur, W=100, path=None):
+    miners = [msim.Miner(k, p[k], q[k], bool(s[k])) for k in range(len(p))]
+    sim = msim.Simulation(miners, dur, total_weight=W)
+    if path is not None:
+        assert sim.pipeline_info(n)["uses_pipeline"] == path
+    res = sim.run(n, 0, seed, 0, per_run=True)
+    f, st, _, _ = oracle.run_batch(p, q, s, dur, n, 0, seed, threads=16, total_weight=W)
+    assert np.array_equal(res.found.astype(np.int64), f), (p, q, s, dur, seed)
+    assert np.array_equal(res.stale.astype(np.int64), st), (p, q, s, dur, seed)
+    assert np.array_equal(res.best_height.astype(np.int64), f.sum(axis=1))
+    return res
+
+
+def test_gpu_general_100_miners_one_selfish(msim, oracle):
+    """A 100-miner network (integer weights, W = 1000) with one selfish miner at 30 %, 1 s delays."""
+    rng = random.Random(5)
+    p = [300] + _rand_weights(99, rng, 700)
+    _vs_oracle(msim, oracle, p, [1000] * 100, [True] + [False] * 99, 64, 77, 7 * DAY, W=1000, path=4)
+
+
+def test_gpu_general_majority_two_selfish(msim, oracle):
+    """Two selfish miners holding 70 % (the entity engine flags these runs; E2 hands them to G)."""
+    _vs_oracle(msim, oracle, [35, 35, 20, 10], [1000] * 4, [True, True, False, False], 64, 4242, 30 * DAY, path=3)
+
+
+def test_gpu_general_selfish_majority_one_miner(msim, oracle):
+    """One selfish miner with 60 % for a year: its lead grows all year, so the runs reach G's last window."""
+    res = _vs_oracle(msim, oracle, [60, 25, 15], [100, 100, 100], [True, False, False], 16, 99, D, path=3)
+    assert res.found[:, 0].min() > 0
+
+
+def test_gpu_general_many_selfish(msim, oracle):
+    """Six selfish miners (the entity engine serves at most four), random networks up to 15 miners."""
+    _vs_oracle(msim, oracle, [10] * 6 + [20, 20], [1000] * 8, [True] * 6 + [False] * 2, 64, 7, 30 * DAY, path=4)
+    rng = random.Random(31)
+    for _ in range(4):
+        m = rng.randint(6, 15)
+        p = _rand_weights(m, rng)
+        s = [k < 5 for k in range(m)]
+        rng.shuffle(s)
+        q = [rng.choice([0, 100, 1000, 10_000]) for _ in range(m)]
+        _vs_oracle(msim, oracle, p, q, s, 32, rng.randrange(2**32), 30 * DAY, path=4)
+
+
+def test_gpu_general_forced_equals_fast_paths(msim, oracle, monkeypatch):
+    """MSIM_FORCE_GENERAL routes BASELINE configs[1] / configs[2] networks onto G: same counters as the
+    oracle (and hence as the pipelines and the entity engine)."""
+    monkeypatch.setenv("MSIM_FORCE_GENERAL", "1")
+    for name in ("c2", "c3"):
+        miners = msim.PRESETS[name]()
+        p = [mm.perc for mm in miners]
+        q = [mm.propagation_ms for mm in miners]
+        s = [mm.is_selfish for mm in miners]
+        _vs_oracle(msim, oracle, p, q, s, 256, 1000, D, path=4)
+
+
+def test_gpu_general_as_e2_fallback(msim, oracle, monkeypatch):
+    """MSIM_SEL_FORCE_RETRY + MSIM_SEL_FORCE_GEN: E1 flags every run, E2 hands every run to G, so G
+    computes the whole configs[2] batch through the fallback lists: bit-exact per run."""
+    monkeypatch.setenv("MSIM_SEL_FORCE_RETRY", "1")
+    monkeypatch.setenv("MSIM_SEL_FORCE_GEN", "1")
+    miners = msim.PRESETS["c3"]()
+    p = [mm.perc for mm in miners]
+    q = [mm.propagation_ms for mm in miners]
+    s = [mm.is_selfish for mm in miners]
+    _vs_oracle(msim, oracle, p, q, s, 512, 1000, D, path=3)
+
+
+def test_gpu_general_sweep(msim, oracle):
+    """A sweep with a point only G serves runs every point on G: per-point per-run counters vs the oracle."""
+    pts = [[msim.Miner(k, w, 1000, k < 5) for k, w in enumerate([10] * 7 + [15, 15])],
+           msim.PRESETS["c3"](), msim.PRESETS["c2"]()]
+    sw = msim.Sweep(pts, 30 * DAY)
+    res = sw.run(32, 0, 500, 0, per_run=True)
+    for i, miners in enumerate(pts):
+        p = [mm.perc for mm in miners]
+        q = [mm.propagation_ms for mm in miners]
+        s = [mm.is_selfish for mm in miners]
+        f, st, _, _ = oracle.run_batch(p, q, s, 30 * DAY, 32, 0, 500, threads=16)
+        assert np.array_equal(res[i].found.astype(np.int64), f), i
+        assert np.array_equal(res[i].stale.astype(np.int64), st), i
