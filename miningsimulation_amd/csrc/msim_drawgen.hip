@@ -107,8 +107,11 @@ struct DevCtx {
     __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * a.gps + g) * a.nr + r] = sum; }
 };
 
+// Resident K1 waves per SIMD the register budget is sized for (VGPRs <= 512 / waves). Measured on MI355X
+// (c2, profiles/r03/INDEX.md): 4 waves (113 VGPRs) 4.17 ms, 5 (96) 4.02 ms, 6 (80) 3.75 ms, 7 (72) 7.3 ms and
+// 8 (64) 13.7 ms, where the spills reach the draw loop's hot values.
 #ifndef MSIM_K1_WAVES
-#define MSIM_K1_WAVES 0
+#define MSIM_K1_WAVES 6
 #endif
 #if MSIM_K1_WAVES
 __global__ __launch_bounds__(256, MSIM_K1_WAVES) void msim_draws_kernel(const DrawArgs a)

@@ -104,17 +104,6 @@ MSIM_HD uint64_t rng_next(Rng &r)  // xoroshiro128++.h:26-34
     return result;
 }
 
-// The state before rng_next(r): the xoroshiro128 update is a bijection, t = s0 ^ s1 = rotr(s1', 28),
-// rotl(s0, 49) = s0' ^ t ^ (t << 21). Lets a draw loop recover an earlier state on a rare path instead
-// of keeping a copy of it live in registers.
-MSIM_HD void rng_prev(Rng &r)
-{
-    const uint64_t t = rotl64(r.s1, 36);
-    const uint64_t s0 = rotl64(r.s0 ^ t ^ (t << 21), 15);
-    r.s0 = s0;
-    r.s1 = t ^ s0;
-}
-
 MSIM_HD int32_t hi_word(double x) { return (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32); }
 MSIM_HD double with_hi_word(double x, uint32_t hi)
 {

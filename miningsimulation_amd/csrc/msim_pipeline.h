@@ -30,6 +30,9 @@
 
 namespace msim {
 
+#ifndef MSIM_K2_NX
+#define MSIM_K2_NX NX_FAST  // K2's extra in-flight blocks (measured: NX_WIDE 150 us vs NX_FAST 141 us per c2 launch)
+#endif
 constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
 constexpr uint32_t MIN_SEG = 512;       // shortest K1 worker (keeps the jump-ahead cost < 5 %)
 constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pairs (<= 16 owners)
@@ -101,7 +104,7 @@ struct PipeArgs {  // K2 / K3
     const GroupRec *grec;
     const EpEntry *list;
     const uint32_t *list_count;
-    uint32_t *recs;       // [lcap][rec_words]: end, flags, F[M], S[M]
+    uint32_t *recs;       // [lcap][rec_words]: end, flags, F[M], S[M], first block
 };
 
 enum : uint32_t { REC_ENDED = 1u, REC_ERR = 2u, REC_SKIP = 4u };
@@ -122,7 +125,7 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     const double need = mu + 8.0 * sd + 64.0;  // blocks to pre-generate (P(more) < 1e-15 per run)
     const uint64_t want = (n_runs + 255) / 256 * 256;
     // slice size first (memory), with an upper estimate of the per-run bytes
-    L.rec_words = 2 + 2 * m;
+    L.rec_words = 3 + 2 * m;
     const double nb_est = need + 2.0 * MIN_SEG;
     const double per_run = 64.0 * (8.0 + CNT_WORDS * 4 + 4) + 4.0 * (rho * nb_est * 2 + 64.0 * 16) +
                            2.0 * nb_est / GROUP * (4.0 + CNT_WORDS * 4 + sizeof(GroupRec)) +
@@ -284,24 +287,22 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
         uint32_t gacc = 0;
         for (uint32_t q4 = 0; q4 < GROUP / 4; ++q4) {
             uint32_t I[4], info[4];
-            if (draw_quad_fast(ri, rp, lt, pt, kc, I, info)) {
-                Rng a = ri, b = rp;  // back to the quad's start (no copy of it stays live)
-                for (int t = 0; t < 4; ++t) {
-                    rng_prev(a);
-                    rng_prev(b);
-                }
-                draw_quad_exact(a, b, lt, pt, I, info);
-            }
+            // The quad's start states are read only on the two rare paths below; at K1's 80-VGPR budget (6
+            // waves per SIMD, msim_drawgen.hip) the compiler keeps them in scratch, written once per quad.
+            // Measured on MI355X: recovering them by inverse stepping instead (no scratch, 84 VGPRs) made K1
+            // 11 % slower at the same occupancy (profiles/r03/INDEX.md, k1 A/B).
+            const Rng ri0 = ri, rp0 = rp;
+            if (draw_quad_fast(ri, rp, lt, pt, kc, I, info)) draw_quad_exact(ri0, rp0, lt, pt, I, info);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 gacc += Icur;
                 const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
                 cx.count(infocur);
                 if (cx.vote(slow)) {
-                    Rng a = ri, b = rp;  // the streams after block i+1: 3 - q steps back from the quad's end
-                    for (int t = q; t < 3; ++t) {
-                        rng_prev(a);
-                        rng_prev(b);
+                    Rng a = ri0, b = rp0;  // the streams after block i+1
+                    for (int t = 0; t <= q; ++t) {
+                        rng_next(a);
+                        rng_next(b);
                     }
                     cx.slow(slow, b0 + g * GROUP + q4 * 4 + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
                             (I[q] << 5) | info_finder(info[q]), a, b);
@@ -340,29 +341,42 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         F[k] = 0;
         S[k] = 0;
     }
-    // 1. Segment containing the end of the run: the first whose last block is found at >= D.
+    // 1. Segment containing the end of the run: the first whose last block is found at >= D. The sums are
+    // loaded KB at a time (independent loads in flight together), then scanned.
+    constexpr uint32_t KB = 8;
     int64_t T = 0;
     int e = -1;
-    for (uint32_t j = 0; j < a.nseg; ++j) {
-        const int64_t ss = (int64_t)a.segsum[(size_t)j * a.nr + r];
-        if (T + ss >= D) {
-            e = (int)j;
-            break;
+    for (uint32_t j0 = 0; j0 < a.nseg && e < 0; j0 += KB) {
+        uint64_t ss[KB];
+#pragma unroll
+        for (uint32_t j = 0; j < KB; ++j) ss[j] = j0 + j < a.nseg ? a.segsum[(size_t)(j0 + j) * a.nr + r] : 0ull;
+#pragma unroll
+        for (uint32_t j = 0; j < KB; ++j) {
+            if (e < 0 && j0 + j < a.nseg) {
+                if (T + (int64_t)ss[j] >= D) e = (int)(j0 + j);
+                else T += (int64_t)ss[j];
+            }
         }
-        T += ss;
-        if (add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr)) return false;  // fell through
     }
     if (e < (int)a.band_lo) return false;  // past the pre-generated draws or outside the band
-    // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153).
+    for (int j = 0; j < e; ++j)
+        if (add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr)) return false;  // fell through
+    // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Group sums
+    // KG at a time, as above (a segment has up to a few hundred groups).
+    constexpr uint32_t KG = 16;
     const size_t gb = (size_t)(e - (int)a.band_lo) * a.gps;
     uint32_t G = a.gps;
-    for (uint32_t g = 0; g < a.gps; ++g) {
-        const int64_t gs = (int64_t)a.gsum[(gb + g) * a.nr + r];
-        if (T + gs >= D) {
-            G = g;
-            break;
+    for (uint32_t g0 = 0; g0 < a.gps && G == a.gps; g0 += KG) {
+        uint32_t gs[KG];
+#pragma unroll
+        for (uint32_t g = 0; g < KG; ++g) gs[g] = g0 + g < a.gps ? a.gsum[(gb + g0 + g) * a.nr + r] : 0u;
+#pragma unroll
+        for (uint32_t g = 0; g < KG; ++g) {
+            if (G == a.gps && g0 + g < a.gps) {
+                if (T + (int64_t)gs[g] >= D) G = g0 + g;
+                else T += (int64_t)gs[g];
+            }
         }
-        T += gs;
     }
     if (G == a.gps) return false;
     if (add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr)) return false;
@@ -411,13 +425,13 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         for (uint32_t c = 0; c < ns; ++c) {
             const uint32_t idx = a.slots[((size_t)j * a.cap + c) * a.nr + r];
             if (idx >= a.lcap) return false;
-            const uint32_t s = a.list[idx].block;
+            const uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
+            const uint32_t s = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
             if (s >= n_end) {  // no later episode starts before the end of the run
                 stop = true;
                 break;
             }
             if (s < cursor) continue;  // consumed by the previous episode
-            const uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
             const uint32_t fl = rec[1];
             if (fl & (REC_ERR | REC_SKIP)) return false;
 #pragma unroll
@@ -454,6 +468,7 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
 {
     const EpEntry e = a.list[idx];
     uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
+    rec[2 + 2 * M] = e.block;
     const uint32_t seg = e.block / a.seg;
     int64_t T = (int64_t)e.offset;
     for (uint32_t j = 0; j < seg; ++j) T += (int64_t)a.segsum[(size_t)j * a.nr + e.run];
@@ -471,7 +486,9 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     src.cur = e.w0;
     src.nxt = e.w1;
     src.have_nxt = true;
-    Sim<M, false, true, NX_WIDE, NG_WIDE> s;
+    // K2's capacities: MSIM_K2_NX extra in-flight blocks (an episode that needs more flags its run, which
+    // the retry kernel recomputes with NX_WIDE), deep branches on
+    Sim<M, false, true, MSIM_K2_NX, NG_FAST> s;
     EpisodeOut<M> o;
     s.episode(p, src, T, o);
     rec[0] = o.end;

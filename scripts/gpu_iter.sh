@@ -22,6 +22,7 @@ for v in $VARIANTS; do
 done
 if [ -n "$PROF" ]; then
   c=${PROF%:*}; s=${PROF#*:}
+  [ -n "$PROFLIB" ] && export MSIM_LIB=$PWD/miningsimulation_amd/variants/libmsim_$PROFLIB.so
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof -- python3 bench.py --config $c --streams $s --steps 10 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
-  find $O/prof -name "*kernel_stats.csv" | head -3
+  python3 scripts/rocprof_summary.py $O/prof | head -8
 fi

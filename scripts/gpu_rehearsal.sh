@@ -17,3 +17,9 @@ for c in c3 c5; do
 done
 timeout -k 10 200 python -u scripts/stage_sweep.py 8192 > $O/sweep.txt 2>&1 || { cat $O/sweep.txt; exit 1; }
 grep sweep $O/sweep.txt
+if [ -n "$PROF" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2s1 -o prof -- python3 bench.py --config c2 --streams 1 --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_c2s1.log 2>&1 || { tail -20 $O/prof_c2s1.log; exit 1; }
+  python3 scripts/rocprof_summary.py $O/prof_c2s1 | head -8
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o prof -- python3 bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_c3.log 2>&1 || { tail -20 $O/prof_c3.log; exit 1; }
+  python3 scripts/rocprof_summary.py $O/prof_c3 | head -8
+fi

@@ -5,7 +5,6 @@ G serves every network with selfish miners that the entity engine does not (more
 selfish miner in a network of more than 15 miners) and finishes the runs the entity engine cannot (a
 selfish majority whose withheld chain outgrows the 16-height window). These are exactly the networks
 round 2 rejected with MSIM_E_SELFISH / MSIM_E_CAPACITY (Missing #1-#2, Weak #10)."""
-import os
 import random
 
 import numpy as np
@@ -61,9 +60,9 @@ def test_gpu_general_majority_two_selfish(msim, oracle):
 
 
 def test_gpu_general_selfish_majority_one_miner(msim, oracle):
-    """One selfish miner with 60 % for a year: its lead grows all year, so the runs reach G's last window."""
-    res = _vs_oracle(msim, oracle, [60, 25, 15], [100, 100, 100], [True, False, False], 16, 99, D, path=3)
-    assert res.found[:, 0].min() > 0
+    """One selfish miner with 60 % for a year: its lead grows all year, so the runs reach G's last window
+    (a run whose selfish miner never has to reveal ends with none of its blocks in the best chain)."""
+    _vs_oracle(msim, oracle, [60, 25, 15], [100, 100, 100], [True, False, False], 16, 99, D, path=3)
 
 
 def test_gpu_general_many_selfish(msim, oracle):
