@@ -115,24 +115,34 @@ __device__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogTab *
 }  // namespace
 
 // ---------------------------------------------------------------- W1
-__global__ __launch_bounds__(256) void msim_wide_draws_kernel(const WideArgs a)
+// W1_RUNS runs (waves) per workgroup share one copy of the pick tables in LDS; W1_WAVES is the resident waves
+// per SIMD the register budget is sized for. The LDS per workgroup ((m+1)*8 + 8 KiB tables + W1_RUNS * 4m
+// histograms) and the VGPRs together set the occupancy.
+#ifndef W1_RUNS
+#define W1_RUNS 4
+#endif
+#ifndef W1_WAVES
+#define W1_WAVES 1
+#endif
+constexpr uint32_t W1_TPB = 64 * W1_RUNS;
+__global__ __launch_bounds__(W1_TPB) __attribute__((amdgpu_waves_per_eu(W1_WAVES, 8))) void msim_wide_draws_kernel(const WideArgs a)
 {
     extern __shared__ uint64_t sh64[];
     __shared__ LogTab s_log;
-    __shared__ uint32_t s_cc[4];
+    __shared__ uint32_t s_cc[W1_RUNS];
     const uint32_t m = a.m, tid = threadIdx.x;
     uint64_t *s_cf = sh64;                                    // [m + 1]
     uint16_t *s_bkt = (uint16_t *)(sh64 + m + 1);             // [WB_N]
-    uint32_t *s_hist = (uint32_t *)(s_bkt + WB_N);            // [4][m]
-    for (uint32_t i = tid; i <= m; i += 256) s_cf[i] = a.cf[i];
-    for (uint32_t i = tid; i < WB_N; i += 256) s_bkt[i] = a.bucket[i];
-    for (uint32_t i = tid; i < 4 * m; i += 256) s_hist[i] = 0;
-    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&s_log)[i] = ((const double *)a.logt)[i];
-    if (tid < 4) s_cc[tid] = 0;
+    uint32_t *s_hist = (uint32_t *)(s_bkt + WB_N);            // [W1_RUNS][m]
+    for (uint32_t i = tid; i <= m; i += W1_TPB) s_cf[i] = a.cf[i];
+    for (uint32_t i = tid; i < WB_N; i += W1_TPB) s_bkt[i] = a.bucket[i];
+    for (uint32_t i = tid; i < W1_RUNS * m; i += W1_TPB) s_hist[i] = 0;
+    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += W1_TPB) ((double *)&s_log)[i] = ((const double *)a.logt)[i];
+    if (tid < W1_RUNS) s_cc[tid] = 0;
     __syncthreads();
 
     const uint32_t w = tid >> 6, lane = tid & 63u;
-    const uint32_t r = blockIdx.x * 4 + w;  // slice-local run
+    const uint32_t r = blockIdx.x * W1_RUNS + w;  // slice-local run
     if (r >= a.n) return;                   // wave-uniform; no block barrier below
     const W1Lds s{s_cf, s_bkt, s_hist + w * m, s_cc + w};
     const uint64_t run = a.run_begin + r;
@@ -456,7 +466,7 @@ __global__ void msim_wide_pick_kernel(const uint64_t *__restrict__ cf, const uin
 }
 
 // ---------------------------------------------------------------- host side
-size_t wide_w1_lds(uint32_t m) { return ((size_t)m + 1) * 8 + (size_t)WB_N * 2 + 4 * (size_t)m * 4; }
+size_t wide_w1_lds(uint32_t m) { return ((size_t)m + 1) * 8 + (size_t)WB_N * 2 + W1_RUNS * (size_t)m * 4; }
 size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch)
 {
     return (size_t)4 * m * 8 + 4 * ((size_t)2 * m + 3 * (size_t)rcap + (size_t)(1 + nch) * 64) * 4;
@@ -496,7 +506,7 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
             (void)hipEventRecord(eb, s);
         }
         if (hipMemsetAsync(a.counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
-        hipLaunchKernelGGL(msim_wide_draws_kernel, dim3((cn + 3) / 4), dim3(256), l1, s, a);
+        hipLaunchKernelGGL(msim_wide_draws_kernel, dim3((cn + W1_RUNS - 1) / W1_RUNS), dim3(W1_TPB), l1, s, a);
         if (ee) (void)hipEventRecord(ee, s);
         // W2 grid: ~rho * blocks candidates per run, grid-stride beyond 16 384 workgroups
         const double est = (double)cn * a.rcap * 0.6;
