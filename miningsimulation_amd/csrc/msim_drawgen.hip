@@ -53,16 +53,32 @@ __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rn
 // and lane, [owner][lane]: conflict-free, and the increment is one ds_add_u32 of a constant), wave-
 // aggregated appends to the dense episode list, the band's group records.
 constexpr uint32_t K1_OWNERS = 2 * CNT_WORDS;  // 15 miners + PickFinder's fall-through (index 15)
+constexpr uint32_t K1_NSL = K1_OWNERS;         // LDS row after the owners: the lane's slow-block count
 
+// The slow path keeps no per-lane register across the draw loop: its lane-dependent values are rebuilt from
+// the ballot mask (mbcnt), wave-uniform SGPRs and LDS (the per-lane list count), so the loop's register
+// budget (K1_WAVES below) goes to the draws. Measured on MI355X (profiles/r03/INDEX.md): with the lane id,
+// its bit, the list count and the counter address held across the loop, the compiler reloaded them from
+// scratch once per quad (six scratch loads and two vmcnt(0) waits per quad).
 struct DevCtx {
     const DrawArgs &a;
     uint32_t (*cnt)[256];
     uint64_t amask;  // active lanes of the wave (runs < n)
-    uint32_t tid, lane, r, seg, jb, nsl;
+    uint32_t tid, r0, seg, jb;  // r0: the wave's first run (wave-uniform)
+    uint32_t cbase;             // tid * 4, rebuilt every quad (quad())
+    uint32_t wbase;             // 4 x the wave's first thread (SGPR)
+    __device__ __forceinline__ void quad()
+    {
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshl_add_u32 %0, %0, 2, %1"
+                     : "=&v"(cbase) : "s"(wbase));
+    }
     // owner row k = info_finder(info) sits at byte offset k << 10 = info & (15 << INFO_K_SHIFT)
     __device__ __forceinline__ void count(uint32_t info)
     {
-        atomicAdd((uint32_t *)((char *)&cnt[0][tid] + (info & (15u << INFO_K_SHIFT))), 1u);
+        // the array's base is a constant the compiler folds into the instruction's offset field
+        const uint32_t ad = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)&cnt[0][0] +
+                            ((info & (15u << INFO_K_SHIFT)) | cbase);
+        __atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)ad, 1u, __ATOMIC_RELAXED);
     }
     __device__ __forceinline__ bool vote(bool s) const { return (__builtin_amdgcn_ballot_w64(s) & amask) != 0ull; }
     // the owner counters packed as the u16 pairs of the workspace layout (msim_pipeline.h CNT_WORDS)
@@ -70,13 +86,20 @@ struct DevCtx {
     __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         const uint64_t mask = __builtin_amdgcn_ballot_w64(s) & amask;
-        const int leader = __ffsll((unsigned long long)mask) - 1;
+        // rank of this lane among the slow ones (asm volatile: computed here, not hoisted out of the loop)
+        uint32_t below;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, %1, 0\n\tv_mbcnt_hi_u32_b32 %0, %2, %0"
+                     : "=&v"(below) : "s"((uint32_t)mask), "s"((uint32_t)(mask >> 32)));
+        const bool mine = s & ((amask >> 0) != 0ull);
         uint32_t base = 0;
-        if ((int)lane == leader) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
-        base = __shfl(base, leader, 64);
-        if (!((mask >> lane) & 1ull)) return;
-        const uint32_t idx =
-            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (mine & (below == 0u)) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
+        base = __builtin_amdgcn_readlane(base, (uint32_t)(__ffsll((unsigned long long)mask) - 1));
+        if (!mine) return;
+        uint32_t lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=&v"(lane));
+        if (!((amask >> lane) & 1ull)) return;
+        const uint32_t r = r0 + lane;
+        const uint32_t idx = base + below;
         if (idx < a.lcap) {
             EpEntry e;
             e.run = r;
@@ -89,11 +112,15 @@ struct DevCtx {
             e.rp = rp;
             a.list[idx] = e;
         }
-        if (nsl < a.cap) a.slots[((size_t)seg * a.cap + nsl) * a.nr + r] = idx;
-        ++nsl;
+        uint32_t *nsl = &cnt[K1_NSL][r & 255u];
+        const uint32_t c = *nsl;
+        if (c < a.cap) a.slots[((size_t)seg * a.cap + c) * a.nr + r] = idx;
+        *nsl = c + 1u;
     }
+    __device__ __forceinline__ uint32_t run() const { return r0 + (tid & 63u); }
     __device__ void group_start(uint32_t g, uint32_t w0, const Rng &ri, const Rng &rp)
     {
+        const uint32_t r = run();
         const size_t gi = (size_t)jb * a.gps + g;
         GroupRec gr;
         gr.ri = ri;
@@ -104,7 +131,7 @@ struct DevCtx {
 #pragma unroll
         for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = packed(w);
     }
-    __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * a.gps + g) * a.nr + r] = sum; }
+    __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum; }
 };
 
 // Resident K1 waves per SIMD the register budget is sized for (VGPRs <= 512 / waves). Measured on MI355X
@@ -123,14 +150,14 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     __shared__ struct {
         PickTab pick;
         LogTab log;
-        uint32_t cnt[K1_OWNERS][256];
+        uint32_t cnt[K1_OWNERS + 1][256];
     } sm;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < sizeof(PickTab) / 4; i += 256) ((uint32_t *)&sm.pick)[i] = ((const uint32_t *)a.tab.pick)[i];
     for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&sm.log)[i] = ((const double *)a.tab.logt)[i];
     auto s_cnt = sm.cnt;
 #pragma unroll
-    for (uint32_t w = 0; w < K1_OWNERS; ++w) s_cnt[w][tid] = 0;
+    for (uint32_t w = 0; w <= K1_OWNERS; ++w) s_cnt[w][tid] = 0;
     __syncthreads();
 
     const uint32_t r = blockIdx.x * 256 + tid;  // slice-local run (< nr)
@@ -141,12 +168,14 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
 
     const uint32_t b0 = seg * a.seg;
-    DevCtx cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, tid & 63u, r, seg, seg - a.band_lo, 0u};
+    DevCtx cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, (uint32_t)__builtin_amdgcn_readfirstlane(r & ~63u), seg,
+              seg - a.band_lo, 0u,
+              (uint32_t)__builtin_amdgcn_readfirstlane((tid & ~63u) * 4u)};
     const uint64_t tsum = draw_segment(cx, ri, rp, &sm.log, &sm.pick, b0, a.seg, seg >= a.band_lo);
     a.segsum[(size_t)seg * a.nr + r] = tsum;
 #pragma unroll
     for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = cx.packed(w);
-    a.nslow[(size_t)seg * a.nr + r] = cx.nsl;
+    a.nslow[(size_t)seg * a.nr + r] = s_cnt[K1_NSL][tid];
 }
 
 // D1 (msim_sel_launch.h): every block's packed word for the entity engine. One lane = (run, segment),

@@ -36,6 +36,10 @@ namespace msim {
 constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
 constexpr uint32_t MIN_SEG = 512;       // shortest K1 worker (keeps the jump-ahead cost < 5 %)
 constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pairs (<= 16 owners)
+#ifndef MSIM_K1_QB
+#define MSIM_K1_QB 4  // blocks drawn together by K1 (one exactness branch per batch)
+#endif
+constexpr int K1_QB = MSIM_K1_QB;
 
 struct EpEntry {
     uint32_t run;     // slice-local run
@@ -237,11 +241,11 @@ struct EpSrc {
 // or a PickFinder index the high word cannot settle: ~8e-6 of quads) is redrawn by draw_quad_exact from
 // the streams at its start. Batching four draws lets their table reads be in flight together.
 MSIM_HD bool draw_quad_fast(Rng &ri, Rng &rp, const LogTab *__restrict__ lt, const PickTab *__restrict__ pt,
-                            FdConsts kc, uint32_t (&I)[4], uint32_t (&info)[4])
+                            FdConsts kc, uint32_t (&I)[K1_QB], uint32_t (&info)[K1_QB])
 {
     uint32_t ki = 0, kp = 0;  // largest acceptance keys of the quad
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < K1_QB; ++q) {
         const uint64_t ui = rng_next(ri), up = rng_next(rp);
         uint32_t a, b;
         I[q] = (uint32_t)interval_ms_fast_key(ui, lt, a, kc);
@@ -252,10 +256,10 @@ MSIM_HD bool draw_quad_fast(Rng &ri, Rng &rp, const LogTab *__restrict__ lt, con
     return ki >= FD_OK_RANGE || kp >= PICK_RARE_LO;
 }
 MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, const PickTab *__restrict__ pt,
-                             uint32_t (&I)[4], uint32_t (&info)[4])
+                             uint32_t (&I)[K1_QB], uint32_t (&info)[K1_QB])
 {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < K1_QB; ++q) {
         I[q] = draw_interval(ri, lt);  // the exact glibc sequence stays out of line (interval_ms_exact_dev)
         info[q] = pt->info[pick_q_exact(rng_next(rp))];
     }
@@ -269,6 +273,7 @@ MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, cons
 //                                     (offset = its find time minus the segment's start; its word, the
 //                                     next one and both streams after them)
 //   group(g, sum)                     band only: sum of the group's intervals
+//   quad()                            start of a quad of blocks
 //   group_start(g, w0, ri, rp)        band only: before group g's first block (its word and the streams
 //                                     after it; snapshot the counters)
 // Blocks are drawn four at a time (draw_quad_fast); the streams after a block inside a quad, needed only
@@ -278,23 +283,42 @@ template <class Ctx>
 MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restrict__ lt,
                               const PickTab *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
 {
+#if defined(__HIP_DEVICE_COMPILE__)
+    FdConsts kc{FD_C1, FD_C2, FD_C3, FD_C4, FD_C5};  // all five in SGPRs; c5 reaches a VGPR per quad (below)
+    asm("" : "+s"(kc.c1));
+    asm("" : "+s"(kc.c2));
+    asm("" : "+s"(kc.c3));
+    asm("" : "+s"(kc.c4));
+    asm("" : "+s"(kc.c5));
+#else
     const FdConsts kc = fd_consts();
+#endif
     uint32_t Icur = draw_interval(ri, lt, kc);
     uint32_t infocur = pick_info(rng_next(rp), pt);
     uint64_t tsum = 0;
     for (uint32_t g = 0; g < seg / GROUP; ++g) {
         if (band) cx.group_start(g, (Icur << 5) | info_finder(infocur), ri, rp);
         uint32_t gacc = 0;
-        for (uint32_t q4 = 0; q4 < GROUP / 4; ++q4) {
-            uint32_t I[4], info[4];
+        for (uint32_t q4 = 0; q4 < GROUP / K1_QB; ++q4) {
+            uint32_t I[K1_QB], info[K1_QB];
+            cx.quad();  // per-quad values the context rebuilds rather than holding across the loop
+#if defined(__HIP_DEVICE_COMPILE__)
+            // the polynomial's leading coefficient, a VGPR operand (one VOP3 reads at most one SGPR), copied
+            // from its SGPR each quad (one v_mov_b64) instead of being held across the loop, where the register
+            // budget of K1 sent it to scratch
+            FdConsts kq = kc;
+            asm volatile("v_mov_b64 %0, %1" : "=v"(kq.c5) : "s"(kc.c5));
+#else
+            const FdConsts kq = kc;
+#endif
             // The quad's start states are read only on the two rare paths below; at K1's 80-VGPR budget (6
             // waves per SIMD, msim_drawgen.hip) the compiler keeps them in scratch, written once per quad.
             // Measured on MI355X: recovering them by inverse stepping instead (no scratch, 84 VGPRs) made K1
             // 11 % slower at the same occupancy (profiles/r03/INDEX.md, k1 A/B).
             const Rng ri0 = ri, rp0 = rp;
-            if (draw_quad_fast(ri, rp, lt, pt, kc, I, info)) draw_quad_exact(ri0, rp0, lt, pt, I, info);
+            if (draw_quad_fast(ri, rp, lt, pt, kq, I, info)) draw_quad_exact(ri0, rp0, lt, pt, I, info);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < K1_QB; ++q) {
                 gacc += Icur;
                 const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
                 cx.count(infocur);
@@ -304,7 +328,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
                         rng_next(a);
                         rng_next(b);
                     }
-                    cx.slow(slow, b0 + g * GROUP + q4 * 4 + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
+                    cx.slow(slow, b0 + g * GROUP + q4 * K1_QB + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
                             (I[q] << 5) | info_finder(info[q]), a, b);
                 }
                 Icur = I[q];

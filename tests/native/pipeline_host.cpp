@@ -29,6 +29,7 @@ struct HostCtx {
         cnt[k >> 1] += 1u << (16u * (k & 1u));
     }
     bool vote(bool s) const { return s; }
+    void quad() {}
     void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         if (!s) return;
