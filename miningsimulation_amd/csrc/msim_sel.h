@@ -146,7 +146,7 @@ MSIM_HD bool ent_same_as_p(const Ent &x, const Ent &P)
     return (x.rp == x.rt) & (x.rt == P.rt) & (x.s == P.s) & (x.xo == P.xo) & (x.br == P.br);
 }
 
-// Env: int64_t prop(uint32_t k); uint32_t get(int arr, uint32_t k); void add(int arr, uint32_t k, uint32_t v);
+// Env: int64_t prop(uint32_t k); int64_t prop_tab(uint32_t k) (same value, as a table read); uint32_t get(int arr, uint32_t k); void add(int arr, uint32_t k, uint32_t v);
 //      void set(int arr, uint32_t k, uint32_t v); ColdAct cold(int c); void cold_put(int c, const ColdAct &);
 //      bool fold_vote(bool due)  (fold now: at least `due`; may be true when not due).
 // Src: bool next(uint32_t &interval_ms, uint32_t &finder)  (finder >= M: PickFinder fell through).

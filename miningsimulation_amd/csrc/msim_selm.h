@@ -76,11 +76,16 @@ struct SelFifo {
         pop();
         return true;
     }
-    MSIM_HD void spec()  // settled form: n == 2 here (fill() on every entry into the form)
+    // The settled form's speculative draw in three parts, so that the compiler can overlap the draw's table
+    // reads and arithmetic with the transition it runs beside: spec() (RNG steps, table reads; n == 2 here,
+    // fill() on every entry into the form), spec_b() (arithmetic) and spec_fix() (the rare exact forms).
+    MSIM_HD void spec()
     {
-        d.draw(I2, k2);
+        d.draw_spec_a();
         n = 3u;
     }
+    MSIM_HD void spec_b() { d.draw_spec_b(I2, k2); }
+    MSIM_HD void spec_fix() { d.fix(I2, k2); }
     MSIM_HD void fill()
     {
         if (n == 0u) {
@@ -187,11 +192,12 @@ struct SelMacro {
     template <class Env, class Src>
     MSIM_HD int step(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
     {
+        const int64_t pk = env.prop_tab(k < (uint32_t)M ? k : 0u);  // read before the draw's table reads
         src.spec();
         uint32_t I = 0, kn = 0;
         const bool have = src.peek(I, kn);
         const bool is_s = k == sid;
-        const int64_t thr = is_s ? 0 : env.prop(k) + (w != 0u ? ps : 0);
+        const int64_t thr = is_s ? 0 : pk + (w != 0u ? ps : 0);
         // (F - Ff bounds the honest stale blocks added to stp since the last flush: a lane about to reach
         // 2^16 takes the engine path, whose hand-over flushes)
         const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (F - Ff < 0xFF00u) &
@@ -214,6 +220,8 @@ struct SelMacro {
 #pragma unroll
         for (int i = 0; i < NP; ++i) pend[i] = rs ? 0ull : pend[i];
         env.add(C_F, k < (uint32_t)M ? k : 0u, ok ? 1u : 0u);
+        src.spec_b();  // the speculative draw is completed in I2 / k2 before pop_if can shift it
+        src.spec_fix();
         src.pop_if(ok);
         T += ok ? (int64_t)I : 0;
         k = ok ? kn : k;

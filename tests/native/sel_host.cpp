@@ -19,6 +19,7 @@ struct HostEnv {
     uint32_t c[4][MAXM];
     ColdAct cs[8];
     int64_t prop(uint32_t k) const { return props[k]; }
+    int64_t prop_tab(uint32_t k) const { return props[k]; }
     uint32_t get(int a, uint32_t k) const { return c[a][k]; }
     void add(int a, uint32_t k, uint32_t v) { c[a][k] += v; }
     void set(int a, uint32_t k, uint32_t v) { c[a][k] = v; }
@@ -47,6 +48,14 @@ struct HostDraw {
         while ((int)f < m && cum[f] <= q) ++f;
         k = f;  // == m: fell through (simulation.h:220)
     }
+    uint32_t pI = 0, pk = 0;
+    void draw_spec_a() { draw(pI, pk); }
+    void draw_spec_b(uint32_t &I, uint32_t &k)
+    {
+        I = pI;
+        k = pk;
+    }
+    void fix(uint32_t &, uint32_t &) {}
 };
 using HostSrc = SelFifo<HostDraw>;
 
