@@ -170,10 +170,11 @@ __global__ __launch_bounds__(TPB) void msim_combine_kernel(const SimParams p, co
                                                           uint32_t *__restrict__ err_count, uint32_t *__restrict__ err_list,
                                                           const uint32_t err_cap)
 {
+    __shared__ uint32_t s_ns[K3_SEG_MAX][TPB];  // per-lane list counts of the run's segments (combine_run)
     const uint32_t r = blockIdx.x * TPB + threadIdx.x;
     const bool active = r < n;
     uint32_t F[M], S[M];
-    const bool ok = active ? combine_run<M>(p, a, r, F, S) : false;
+    const bool ok = active ? combine_run<M>(p, a, r, F, S, &s_ns[0][threadIdx.x], TPB) : false;
     uint64_t v[6 * M];
 #pragma unroll
     for (int i = 0; i < 6 * M; ++i) v[i] = 0;

@@ -356,8 +356,11 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 }
 
 // Combine one run r of a slice. Returns false when the run must be recomputed by the retry path.
+// nsw: K3_SEG_MAX words of per-run scratch at stride nss (device: the lane's LDS column).
+constexpr uint32_t K3_SEG_MAX = 32;
 template <int M>
-MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M])
+MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M],
+                         uint32_t *nsw, size_t nss)
 {
     const int64_t D = p.duration_ms;
 #pragma unroll
@@ -387,7 +390,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         if (add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr)) return false;  // fell through
     // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Group sums
     // KG at a time, as above (a segment has up to a few hundred groups).
-    constexpr uint32_t KG = 16;
+    constexpr uint32_t KG = 32;
     const size_t gb = (size_t)(e - (int)a.band_lo) * a.gps;
     uint32_t G = a.gps;
     for (uint32_t g0 = 0; g0 < a.gps && G == a.gps; g0 += KG) {
@@ -440,34 +443,107 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         for (uint32_t q = 1; q < GROUP; ++q) wd = draw_word(ri, rp, a.tab.logt, a.tab.pick);
         klast = wd & 15u;
     }
-    // 3. Episodes in block order; an episode applies when its first block is reached quiet.
+    // 3. Episodes in block order; an episode applies when its first block is reached quiet. The reads are
+    // gathered in three batches (list counts of segments 0..e, their slot indices, the records' headers), so
+    // a run waits for three rounds of memory latency instead of one per segment and two per episode; a run
+    // with more than EP_MAX episodes up to its end segment (never at BASELINE sizes: ~rho * blocks, 9 for
+    // configs[1]) takes the same walk one read at a time.
     uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
-    bool stop = false;
-    for (int j = 0; j <= e && !stop; ++j) {
-        const uint32_t ns = a.nslow[(size_t)j * a.nr + r];
-        if (ns > a.cap) return false;
-        for (uint32_t c = 0; c < ns; ++c) {
-            const uint32_t idx = a.slots[((size_t)j * a.cap + c) * a.nr + r];
-            if (idx >= a.lcap) return false;
-            const uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
-            const uint32_t s = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
-            if (s >= n_end) {  // no later episode starts before the end of the run
-                stop = true;
-                break;
+    constexpr uint32_t EP_MAX = 32, SEG_MAX = K3_SEG_MAX;
+    uint32_t tot = 0;
+    const bool fits = (uint32_t)e < SEG_MAX;
+    if (fits) {
+        uint32_t nsv[SEG_MAX];
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_MAX; ++j) nsv[j] = j <= (uint32_t)e ? a.nslow[(size_t)j * a.nr + r] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_MAX; ++j) {
+            if (nsv[j] > a.cap) return false;
+            tot += nsv[j];
+            nsw[j * nss] = nsv[j];  // read back below at data-dependent positions
+        }
+    }
+    if (fits && tot <= EP_MAX) {
+        uint32_t idx[EP_MAX];
+        {
+            uint32_t j = 0, c = 0, nj = nsw[0];  // (segment, slot) of entry t; nj = count of segment j
+#pragma unroll
+            for (uint32_t t = 0; t < EP_MAX; ++t) {
+                uint32_t v = 0;
+                if (t < tot) {
+                    while (c >= nj) {
+                        ++j;
+                        c = 0;
+                        nj = nsw[j * nss];
+                    }
+                    v = a.slots[((size_t)j * a.cap + c) * a.nr + r];  // issued without waiting for the last
+                    ++c;
+                }
+                idx[t] = v;
             }
-            if (s < cursor) continue;  // consumed by the previous episode
-            const uint32_t fl = rec[1];
-            if (fl & (REC_ERR | REC_SKIP)) return false;
+        }
+        uint32_t st[EP_MAX], en[EP_MAX], fl[EP_MAX];
+#pragma unroll
+        for (uint32_t t = 0; t < EP_MAX; ++t) {
+            st[t] = en[t] = fl[t] = 0;
+            if (t < tot) {
+                if (idx[t] >= a.lcap) return false;
+                const uint32_t *rec = a.recs + (size_t)idx[t] * a.rec_words;
+                st[t] = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
+                en[t] = rec[0];
+                fl[t] = rec[1];
+            }
+        }
+        bool stop = false;
+#pragma unroll
+        for (uint32_t t = 0; t < EP_MAX; ++t) {
+            if (stop || t >= tot) continue;
+            if (st[t] >= n_end) {  // no later episode starts before the end of the run
+                stop = true;
+                continue;
+            }
+            if (st[t] < cursor) continue;  // consumed by the previous episode
+            if (fl[t] & (REC_ERR | REC_SKIP)) return false;
+            const uint32_t *rec = a.recs + (size_t)idx[t] * a.rec_words;
 #pragma unroll
             for (int k = 0; k < M; ++k) {
                 F[k] += rec[2 + k];
                 S[k] += rec[2 + M + k];
             }
-            cursor = rec[0];
-            if (fl & REC_ENDED) {  // the run ended inside this episode
+            cursor = en[t];
+            if (fl[t] & REC_ENDED) {  // the run ended inside this episode
                 cursor = 0xFFFFFFFFu;
                 stop = true;
-                break;
+            }
+        }
+    } else {
+        bool stop = false;
+        for (int j = 0; j <= e && !stop; ++j) {
+            const uint32_t ns = a.nslow[(size_t)j * a.nr + r];
+            if (ns > a.cap) return false;
+            for (uint32_t c = 0; c < ns; ++c) {
+                const uint32_t idx = a.slots[((size_t)j * a.cap + c) * a.nr + r];
+                if (idx >= a.lcap) return false;
+                const uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
+                const uint32_t s0 = rec[2 + 2 * M];
+                if (s0 >= n_end) {
+                    stop = true;
+                    break;
+                }
+                if (s0 < cursor) continue;
+                const uint32_t f0 = rec[1];
+                if (f0 & (REC_ERR | REC_SKIP)) return false;
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    F[k] += rec[2 + k];
+                    S[k] += rec[2 + M + k];
+                }
+                cursor = rec[0];
+                if (f0 & REC_ENDED) {
+                    cursor = 0xFFFFFFFFu;
+                    stop = true;
+                    break;
+                }
             }
         }
     }
@@ -495,7 +571,14 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     rec[2 + 2 * M] = e.block;
     const uint32_t seg = e.block / a.seg;
     int64_t T = (int64_t)e.offset;
-    for (uint32_t j = 0; j < seg; ++j) T += (int64_t)a.segsum[(size_t)j * a.nr + e.run];
+    // the segment sums before the episode's segment, 8 independent loads at a time
+    for (uint32_t j0 = 0; j0 < seg; j0 += 8) {
+        uint64_t ss[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) ss[j] = j0 + j < seg ? a.segsum[(size_t)(j0 + j) * a.nr + e.run] : 0ull;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) T += (int64_t)ss[j];
+    }
     if (T >= p.duration_ms) {  // beyond the end of the run: never applied
         rec[1] = REC_SKIP;
         return;
