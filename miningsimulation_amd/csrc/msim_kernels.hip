@@ -30,6 +30,10 @@ __global__ __launch_bounds__(TPB, 2) void msim_runs_kernel(const SimParams p, co
         const uint32_t c = *list_count;
         lim = c < list_cap ? c : list_cap;
     }
+    if (LIST && blockIdx.x * TPB >= lim) {  // a retry workgroup with no flagged run (the usual case): zero sums
+        for (uint32_t i = threadIdx.x; i < 6 * M; i += TPB) partials[(size_t)blockIdx.x * 6 * M + i] = 0ull;
+        return;
+    }
     const bool active = idx < lim;
     const uint32_t rel = LIST ? (active ? list[idx] : 0u) : idx;  // run offset from run_begin
     uint64_t v[6 * M];
@@ -154,8 +158,12 @@ __global__ __launch_bounds__(TPB, 2) void msim_sweep_kernel(const SimParams *__r
 __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
 
 // K2: one lane per listed non-fast block (msim_pipeline.h episode_entry).
+// Three resident waves per SIMD (168 VGPRs, some spills at the episode's entry) rather than the two that 207
+// spill-free VGPRs allow: measured on MI355X (profiles/r03/k3ab), c2 with two overlapping streams 9.15M ->
+// 9.37M run-years/s, serial unchanged (K2 shares the GPU with the next step's K1 better).
 template <int M>
-__global__ __launch_bounds__(TPB) void msim_episode_kernel(const SimParams p, const PipeArgs a)
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(3, 8))) void msim_episode_kernel(const SimParams p,
+                                                                                                    const PipeArgs a)
 {
     const uint32_t cnt = *a.list_count;
     const uint32_t lim = cnt < a.lcap ? cnt : a.lcap;
