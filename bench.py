@@ -35,15 +35,15 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 
 
 # HBM bytes per launch of the dominant kernel at the default run counts, from rocprofv3 PMC passes
-# (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, separate passes; c2: profiles/r02/pmc_q.md, K1
-# without the per-block word stream; c5: profiles/r01/pmc_f1.md). PMC counters cannot be collected inside
-# this process; these are the recorded values of the same command.
-TRAFFIC_PMC = {("c2", 32768): 4.09e8, ("c5", 65536): 9.128e8}
-TRAFFIC_SRC = {"c2": "profiles/r02/pmc_q.md", "c5": "profiles/r01/pmc_f1.md"}
+# (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, separate passes; c2: profiles/r03/final/pmc_final.md,
+# K1 of round 3; c5: profiles/r01/pmc_f1.md). PMC counters cannot be collected inside this process; these
+# are the recorded values of the same command.
+TRAFFIC_PMC = {("c2", 32768): 4.98e8, ("c5", 65536): 9.128e8}
+TRAFFIC_SRC = {"c2": "profiles/r03/final/pmc_final.md", "c5": "profiles/r01/pmc_f1.md"}
 # SQ_INSTS_VALU (wave instructions) per launch of the kernels the live timing covers, same passes
-# (c2: K1 only, timed by k1_ms; c3: D1 + E1 = the whole launch, timed by kernel_ms): the counter-based
+# (c2: K1 only, timed by k1_ms; c3: E1 = the whole launch, timed by kernel_ms): the counter-based
 # VALU issue fraction = instructions x 64 lanes / time / peak, reported beside the SURVEY 8(d) convention.
-VALU_INSTS_PMC = {("c2", 32768): (2.269e9, "k1"), ("c3", 131072): (8.241e9 + 2.350e10, "launch"),
+VALU_INSTS_PMC = {("c2", 32768): (1.778e9, "k1"), ("c3", 131072): (2.526e10, "launch"),
                   ("c5", 65536): (5.81e9, "k1")}
 
 
@@ -330,7 +330,7 @@ def main() -> None:
         insts, which = VALU_INSTS_PMC[(args.config, n)]
         t_s = (k1_ms if which == "k1" else kern_ms) / 1e3
         issue_frac = round(insts * 64 / t_s / VALU_PEAK_LANE_OPS, 4) if t_s > 0 else None
-        issue_src = (f"SQ_INSTS_VALU {insts:.4g} per launch (profiles/r02/pmc_q.md, counters_s.md) x 64 lanes / live "
+        issue_src = (f"SQ_INSTS_VALU {insts:.4g} per launch (profiles/r03/final/pmc_final.md) x 64 lanes / live "
                      f"{'K1' if which == 'k1' else 'launch'} time / peak")
     runs_total = args.steps * n * world
     value = runs_total / elapsed
