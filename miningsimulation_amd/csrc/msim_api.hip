@@ -422,6 +422,7 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
 struct SelGroupDev {
     uint32_t nscls, nlist;
     const uint32_t *plist;
+    uint32_t uni;  // every point of the group has a uniform propagation delay
 };
 
 // The slice loop of one launch: D1 (words) -> E1 per group -> E2 (retries) -> F.
@@ -492,6 +493,7 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
             if (!g.nlist) continue;
             a.plist = g.plist;
             a.nlist = g.nlist;
+            a.uni = g.uni;
             if (launch_sel(a, m, g.nscls, s) != hipSuccess) return MSIM_E_HIP;
         }
         event(engine_events);
@@ -903,7 +905,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         msim::WordArgs da;
         rc = sel_word_args(c, cfg->sp, w, &da);
         if (rc) return rc;
-        std::vector<SelGroupDev> groups{{msim::sel_ns_class(cfg->sp.ns), 1u, plist}};
+        std::vector<SelGroupDev> groups{{msim::sel_ns_class(cfg->sp.ns), 1u, plist, cfg->sp.uniform_prop != 0 ? 1u : 0u}};
         Timing &tm = timing();
         std::unique_lock<std::mutex> lk(tm.mu);
         hipEvent_t lb = nullptr, le = nullptr;
@@ -1224,7 +1226,9 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
         std::vector<SelGroupDev> groups;
         const uint32_t *pl = (const uint32_t *)((const char *)d + pb);
         for (const auto &gr : sm->groups) {
-            groups.push_back({gr.nscls, (uint32_t)gr.points.size(), pl});
+            uint32_t uni = 1;
+            for (uint32_t p : gr.points) uni &= sm->sps[p].uniform_prop != 0 ? 1u : 0u;
+            groups.push_back({gr.nscls, (uint32_t)gr.points.size(), pl, uni});
             pl += gr.points.size();
         }
         msim::WordArgs da;

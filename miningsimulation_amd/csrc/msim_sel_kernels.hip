@@ -20,9 +20,11 @@ namespace msim {
 // ------------------------------------------------------------------ entity engine (msim_sel.h)
 // Per-lane counters of the engine in LDS, [array][miner][lane]: lanes of a wave hit distinct banks for any
 // mix of miner indices.
-template <int M>
 // Counter increments are LDS atomics whose result is unused (ds_add_u32): the lane never waits on them.
-// A network whose miners share one propagation delay (every BASELINE config) reads it from a scalar.
+// A network whose miners share one propagation delay (every BASELINE config) reads it from a scalar: in the
+// engine through a wave-uniform branch (uni), in the settled form at compile time (UNI; measured on MI355X:
+// the table read it replaces cost 2.3 % of configs[2], profiles/r03/e1ab/uni_*).
+template <int M, bool UNI = false>
 struct SelDevEnv {
     uint32_t *c;          // &s_cnt[0][tid]
     const int64_t *pr;    // propagation per miner (LDS or global)
@@ -34,7 +36,7 @@ struct SelDevEnv {
     __device__ __forceinline__ void cold_put(int i, const ColdAct &r) { cb[(size_t)i * cstride] = r; }
     __device__ __forceinline__ int64_t prop(uint32_t k) const { return uni ? uprop : pr[k]; }
     // the settled form's read: always the table (no branch), issued at the top of a step
-    __device__ __forceinline__ int64_t prop_tab(uint32_t k) const { return pr[k]; }
+    __device__ __forceinline__ int64_t prop_tab(uint32_t k) const { return UNI ? uprop : pr[k]; }
     __device__ __forceinline__ uint32_t get(int a, uint32_t k) const { return c[(a * M + (int)k) * TPB]; }
     __device__ __forceinline__ void add(int a, uint32_t k, uint32_t v) { atomicAdd(&c[(a * M + (int)k) * TPB], v); }
     __device__ __forceinline__ void set(int a, uint32_t k, uint32_t v) { c[(a * M + (int)k) * TPB] = v; }
@@ -457,11 +459,11 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
 
 // E1: one lane per (point, run of the slice); workgroups never straddle points. FAST: the lane makes its
 // draws itself (SelFastDraw); otherwise it reads the slice's word stream written by D1 (sweeps).
-template <int M, int NS, int NA, int NG, int NQ, int NC, bool FAST, class Src>
+template <int M, int NS, int NA, int NG, int NQ, int NC, bool FAST, bool UNI, class Src>
 __device__ __forceinline__ void sel_lane(const SelArgs &a, const SelParams *P, Src &src, SelOut &o, uint32_t *s_cnt_lane,
                                          const int64_t *s_prop, uint32_t *mcs, size_t lane)
 {
-    SelDevEnv<M> env{s_cnt_lane, s_prop, P->prop[0], P->uniform_prop != 0, a.cold + lane, a.cold_lanes};
+    SelDevEnv<M, UNI> env{s_cnt_lane, s_prop, P->prop[0], P->uniform_prop != 0, a.cold + lane, a.cold_lanes};
     const int64_t D = P->duration_ms;
     if (a.force_retry) {
         o.err = SERR_CAP;
@@ -481,7 +483,7 @@ __device__ __forceinline__ void sel_lane(const SelArgs &a, const SelParams *P, S
     }
 }
 
-template <int M, int NS, int NA, int NG, int NQ, int NC, bool FAST>
+template <int M, int NS, int NA, int NG, int NQ, int NC, bool FAST, bool UNI>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_sel_kernel(const SelArgs a)
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
@@ -528,7 +530,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
             src.d.kc = fd_consts();
             src.d.wt = P->W != 100u;
             src.n = 0;
-            sel_lane<M, NS, NA, NG, NQ, NC, FAST>(a, P, src, o, &s_cnt[0][tid], s_prop, &s_mc[0][tid], lane);
+            sel_lane<M, NS, NA, NG, NQ, NC, FAST, UNI>(a, P, src, o, &s_cnt[0][tid], s_prop, &s_mc[0][tid], lane);
         } else {
             SelWordSrc<M> src;
             src.p = reinterpret_cast<const uint4 *>(a.words) + (size_t)lr * (SEL_TILE / 4);
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
             src.lut = s_lut;
 #endif
             src.init(P->ccum);
-            sel_lane<M, NS, NA, NG, NQ, NC, FAST>(a, P, src, o, &s_cnt[0][tid], s_prop, &s_mc[0][tid], lane);
+            sel_lane<M, NS, NA, NG, NQ, NC, FAST, UNI>(a, P, src, o, &s_cnt[0][tid], s_prop, &s_mc[0][tid], lane);
         }
         if (o.err) {
             const uint32_t pos = atomicAdd(a.counts, 1u);
@@ -623,12 +625,15 @@ static hipError_t launch_sel_ns(const SelArgs &a, hipStream_t s)
     // one selfish miner: the mixed schedule, whose engine episodes are local (one hot slot of each kind
     // flags no run of the configs[3] grid, tests/test_sel_host.py)
     const bool fast = a.words == nullptr;
-    if constexpr (NS == 1) {
-        if (fast) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, true>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-        else hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, false>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-    } else {
-        if (fast) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC, true>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
-        else hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC, false>), dim3(a.nlist * wps), dim3(TPB), 0, s, a);
+    const dim3 grid(a.nlist * wps);
+    if constexpr (NS == 1) {  // the settled form reads the pending finder's delay: a uniform network's from a scalar
+        if (fast && a.uni) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, true, true>), grid, dim3(TPB), 0, s, a);
+        else if (fast) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, true, false>), grid, dim3(TPB), 0, s, a);
+        else if (a.uni) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, false, true>), grid, dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((msim_sel_kernel<M, NS, 1, 4, 1, SEL_NC, false, false>), grid, dim3(TPB), 0, s, a);
+    } else {  // the engine alone (no settled form)
+        if (fast) hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC, true, false>), grid, dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((msim_sel_kernel<M, NS, 2, 4, 2, SEL_NC, false, false>), grid, dim3(TPB), 0, s, a);
     }
     return hipGetLastError();
 }

@@ -92,6 +92,7 @@ struct SelArgs {
     size_t cold_lanes;
     uint32_t *gen_list;     // runs E2 could not finish, for G (msim_general_launch.h), or null: counted as failed
     uint32_t force_gen;     // test switch (MSIM_SEL_FORCE_GEN): E2 hands every run it gets to G
+    uint32_t uni;           // every point of this E1 launch has one propagation delay for all miners
 };
 
 struct SelLayout {
