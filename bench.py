@@ -197,8 +197,8 @@ class _StubSim:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5", "default"])
     ap.add_argument("--runs", type=int, default=0,
                     help="runs per GPU per step (0: 32768 = SIM_RUNS; c3: 131072 = configs[2]'s 1M runs / 8 GPUs; c5: 65536)")
