@@ -204,8 +204,8 @@ def main() -> None:
                     help="runs per GPU per step (0: 32768 = SIM_RUNS; c3: 131072 = configs[2]'s 1M runs / 8 GPUs; c5: 65536)")
     ap.add_argument("--seed-base", type=int, default=1000)
     ap.add_argument("--streams", type=int, default=0,
-                    help="HIP streams the steps alternate over (1: serial; 0: 2 for honest networks, whose "
-                         "latency-bound tail kernels overlap the next draw kernel, 1 for selfish ones)")
+                    help="HIP streams the steps alternate over (1: serial; 0 = 2: an honest step's latency-bound "
+                         "tail kernels, and a selfish launch's last engine waves, overlap the next step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-runs", type=int, default=0, help="0 = auto (~15 s of CPU work)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # tests: CPU stand-in, gloo
@@ -268,7 +268,9 @@ def main() -> None:
     # own workspace and sums, so one step's latency-bound tail kernels (episodes, combine, finalize) and
     # all-reduce overlap the next step's draw kernel. Every step still runs to completion inside the timed
     # region (both sides bracketed by barrier + synchronize).
-    ns = args.streams if args.streams > 0 else (2 if sim.pipeline_info(n).get("uses_pipeline") in (1, 2) else 1)
+    # Two streams for every network (measured on MI355X: c2 7.4 -> 8.7 M in round 2; c3 2.29 -> 2.36 M in round 3,
+    # profiles/r03/e1ab/c3_s*.json: the last waves of one E1 launch overlap the first of the next).
+    ns = args.streams if args.streams > 0 else 2
     lanes = []
     for j in range(ns):
         st = None if args.stub else (torch.cuda.current_stream(dev) if ns == 1 else torch.cuda.Stream(dev))
