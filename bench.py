@@ -145,31 +145,44 @@ def free_port() -> int:
         return sk.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv: list[str]) -> int:
+def spawn_ranks(n: int, argv: list[str], timeout_s: float = 1800.0) -> int:
     """Start ranks 0..n-1 of this script (one process per GPU) and relay rank 0's stdout. The parent never
-    imports torch or touches HIP: each child initialises its own device."""
+    imports torch or touches HIP: each child initialises its own device. Every rank is polled: the first
+    rank to fail (or the overall time limit) ends the job, and the remaining ranks, rank 0 included, are
+    killed, so a rank stuck in a collective whose peer died cannot hang the parent."""
+    import tempfile
+
     port = free_port()
     procs = []
+    out0 = tempfile.TemporaryFile(mode="w+")  # rank 0's stdout (a file: no pipe to drain while polling)
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
-    out = procs[0].communicate()[0]
-    codes = [procs[0].returncode]
-    for p in procs[1:]:
-        try:
-            codes.append(p.wait(timeout=120))
-        except subprocess.TimeoutExpired:
-            p.kill()
-            codes.append(p.wait())
-    if any(c != 0 for c in codes):
-        print(f"bench.py: rank exit codes {codes}", file=sys.stderr)
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL, text=True))
+    t_end = time.monotonic() + timeout_s
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with {bad[0][1]}"
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > t_end:
+            failed = f"time limit {timeout_s:.0f} s"
+            break
+        time.sleep(0.2)
+    if failed:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+        codes = [p.wait() for p in procs]
+        print(f"bench.py: {failed}; rank exit codes {codes}", file=sys.stderr)
         return 1
-    for ln in out.splitlines():  # the JSON line to stdout; library chatter (gloo/RCCL banners) to stderr
+    out0.seek(0)
+    for ln in out0.read().splitlines():  # the JSON line to stdout; library chatter (gloo/RCCL banners) to stderr
         print(ln, file=sys.stdout if ln.startswith("{") else sys.stderr, flush=True)
     return 0
 
@@ -226,6 +239,8 @@ def main() -> None:
         dev = torch.device("cpu")
         if world > 1:
             dist.init_process_group("gloo")
+        if os.environ.get("MSIM_BENCH_STUB_FAIL_RANK") == str(rank):  # tests: a rank dying mid-job
+            raise SystemExit(3)
     else:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)

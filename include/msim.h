@@ -33,7 +33,8 @@ extern "C" {
 #define MSIM_E_WEIGHTS (-2)  /* weights do not add up to 100 (or total_weight): the reference asserts */
 #define MSIM_E_SELFISH (-3)  /* reserved (round 2 rejected selfish networks the entity engine cannot serve;
                                 every network with selfish miners now runs, those on the general engine) */
-#define MSIM_E_MINERS (-4)   /* too many miners (see MSIM_MAX_*_MINERS), or duplicate miner ids */
+#define MSIM_E_MINERS (-4)   /* network too large for the general engine: one run's explicit chains (miners x
+                                blocks a run can have x 12 B) would exceed 8 GiB of device memory */
 #define MSIM_E_HIP (-5)      /* HIP runtime error (no device, launch failure, out of memory) */
 #define MSIM_E_CAPACITY (-6) /* a run outgrew every window of the general engine (its last window holds every
                                 block a run of the config's duration can have: practically never) */
@@ -42,7 +43,8 @@ extern "C" {
 #define MSIM_MAX_MINERS 15        /* networks on the compact per-lane / entity-engine state */
 #define MSIM_MAX_SELFISH 4        /* selfish miners per network on the entity engine (msim_sel.h); more run on
                                      the general engine (msim_general.h) */
-#define MSIM_MAX_WIDE_MINERS 4096 /* honest networks (large-network pipeline, BASELINE configs[4]) */
+#define MSIM_MAX_WIDE_MINERS 4096 /* honest networks on the large-network pipeline (BASELINE configs[4]); larger
+                                     honest networks run on the general engine */
 
 typedef struct msim_miner {
     uint32_t id;            /* Miner::id (simulation.h:43) */
@@ -86,7 +88,10 @@ int msim_config_create(const msim_miner *miners, uint32_t n, int64_t duration_ms
  * on the entity engine; every other network with selfish miners (more selfish miners, or more miners) runs
  * on the general engine (msim_general.h: the reference's explicit chains in bounded windows of device
  * memory, slower per block, exact), which also finishes the runs the entity engine cannot (a selfish
- * majority whose withheld chain outgrows its window). */
+ * majority whose withheld chain outgrows its window). The general engine also serves honest networks of
+ * more than MSIM_MAX_WIDE_MINERS miners and every network whose ids are not distinct or include UINT_MAX
+ * (Genesis's id, simulation.h:31-33): the reference identifies blocks, stale blocks and found blocks by
+ * Miner::id (simulation.h:35-38, 133; main.cpp:24-26), and so does that engine. */
 int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t total_weight,
                                 msim_config **out);
 /* 1 when the config runs on the large-network pipeline (set MSIM_FORCE_WIDE=1 in the environment before
@@ -107,8 +112,9 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
 /* Several GPUs of one node (the std::async loop of main.cpp:205-220 across devices): runs
  * [run_begin, run_begin + n_runs) cut into contiguous shards, one per device in `devices` (NULL = devices
  * 0 .. n_devices - 1), each through msim_launch on its own stream (all devices run concurrently), then ONE
- * ncclAllReduce (RCCL over xGMI, single-process communicator from ncclCommInitAll, issued for every device
- * inside one group) of the integer msim_sums. Every device's buffers are allocated before anything runs, so
+ * ncclAllReduce (RCCL over xGMI, single-process communicator from ncclCommInitAll, created once per device
+ * list and kept for the process, issued for every device inside one group; none for one device) of the
+ * integer msim_sums. Every device's buffers are allocated before anything runs, so
  * an allocation failure returns MSIM_E_HIP without entering a collective. The result is bit-identical to
  * msim_run for every n_devices (out_sums from the fixed-point sums; opt_sums or NULL). */
 int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,

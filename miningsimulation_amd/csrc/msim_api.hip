@@ -31,7 +31,25 @@ struct GenHost {
     std::vector<uint64_t> w;
     std::vector<int64_t> prop;
     std::vector<uint8_t> self;
+    std::vector<uint32_t> ids;  // Miner::id (msim_general.h: blocks are identified by id class)
 };
+
+// Id classes of a miner list (msim_general.h GenParams::cls): the lowest index with the same id; the class
+// of id UINT_MAX (Genesis's id, simulation.h:31-33) or GEN_GENESIS.
+static void gen_id_classes(const std::vector<uint32_t> &ids, std::vector<uint32_t> &cls, uint32_t *umax)
+{
+    const size_t m = ids.size();
+    std::vector<uint32_t> ord(m);
+    for (size_t k = 0; k < m; ++k) ord[k] = (uint32_t)k;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
+    cls.assign(m, 0);
+    *umax = msim::GEN_GENESIS;
+    for (size_t i = 0; i < m; ++i) {
+        const uint32_t k = ord[i];
+        cls[k] = (i > 0 && ids[ord[i - 1]] == ids[k]) ? cls[ord[i - 1]] : k;  // stable: the lowest index first
+        if (ids[k] == 0xFFFFFFFFu) *umax = cls[k];
+    }
+}
 
 struct msim_config {
     msim::SimParams p;
@@ -529,7 +547,7 @@ int gen_tables_upload(const std::vector<const GenHost *> &hs, void **out)
     std::vector<size_t> o(np);
     for (size_t i = 0; i < np; ++i) {
         o[i] = off;
-        off = al(off + hs[i]->w.size() * 17);
+        off = al(off + hs[i]->w.size() * 21);
     }
     std::vector<char> h(off, 0);
     void *d = nullptr;
@@ -539,20 +557,27 @@ int gen_tables_upload(const std::vector<const GenHost *> &hs, void **out)
         const size_t m = g.w.size();
         uint64_t *cum = (uint64_t *)(h.data() + o[i]);
         int64_t *prop = (int64_t *)(h.data() + o[i] + 8 * m);
-        uint8_t *self = (uint8_t *)(h.data() + o[i] + 16 * m);
+        uint32_t *cls = (uint32_t *)(h.data() + o[i] + 16 * m);
+        uint8_t *self = (uint8_t *)(h.data() + o[i] + 20 * m);
+        std::vector<uint32_t> cv;
+        uint32_t umax = msim::GEN_GENESIS;
+        gen_id_classes(g.ids, cv, &umax);
         uint64_t c = 0;
         for (size_t k = 0; k < m; ++k) {
             cum[k] = (c += g.w[k]);
             prop[k] = g.prop[k];
+            cls[k] = cv[k];
             self[k] = g.self[k];
         }
         msim::GenParams *gp = (msim::GenParams *)h.data() + i;
         gp->duration_ms = g.duration_ms;
         gp->mult = 0xFFFFFFFFFFFFFFFFull / g.W;
         gp->m = (uint32_t)m;
+        gp->umax = umax;
         gp->cum = (const uint64_t *)((char *)d + o[i]);
         gp->prop = (const int64_t *)((char *)d + o[i] + 8 * m);
-        gp->self = (const uint8_t *)((char *)d + o[i] + 16 * m);
+        gp->cls = (const uint32_t *)((char *)d + o[i] + 16 * m);
+        gp->self = (const uint8_t *)((char *)d + o[i] + 20 * m);
     }
     if (hipMemcpy(d, h.data(), off, hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d);
@@ -670,14 +695,19 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
                        msim_config **out)
 {
     if (!miners || !out || n == 0 || duration_ms < 0 || total_weight == 0) return MSIM_E_INVALID;
-    if (n > msim::WIDE_MAX_M) return MSIM_E_MINERS;
     if (total_weight >= (1ull << 31)) return MSIM_E_WEIGHTS;
+    // Ids only name a block's creator (simulation.h:22-38); the fast engines count blocks per miner INDEX,
+    // which is the reference's per-id count exactly when every id is distinct and none is Genesis's id
+    // UINT_MAX (simulation.h:31-33). Any other network (two miners sharing an id: shared blocks, stale
+    // counting and found counts, main.cpp:24-26, simulation.h:133; an id UINT_MAX: Genesis counted as its
+    // block) runs on the general engine, whose chains hold id classes (msim_general.h).
+    bool id_quirk = false;
     {
         std::vector<uint32_t> ids(n);
         for (uint32_t k = 0; k < n; ++k) ids[k] = miners[k].id;
         std::sort(ids.begin(), ids.end());
-        for (uint32_t k = 1; k < n; ++k)
-            if (ids[k] == ids[k - 1]) return MSIM_E_MINERS;
+        for (uint32_t k = 1; k < n; ++k) id_quirk = id_quirk || ids[k] == ids[k - 1];
+        id_quirk = id_quirk || ids[n - 1] == 0xFFFFFFFFu;
     }
     uint64_t total = 0;
     uint32_t nself = 0;
@@ -694,8 +724,12 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     // The entity engine takes up to SEL_MAXS selfish miners in networks of up to MSIM_MAX_MINERS miners; any
     // other network with selfish miners runs on the general engine (msim_general.h), as does any network when
     // MSIM_FORCE_GENERAL is set (test switch).
-    const bool gen = nself > (uint32_t)msim::SEL_MAXS || (nself && n > MSIM_MAX_MINERS) ||
-                     getenv("MSIM_FORCE_GENERAL") != nullptr;
+    // Honest networks of more than WIDE_MAX_M miners (beyond the large-network pipeline's LDS tables) also
+    // run on G.
+    const bool gen = nself > (uint32_t)msim::SEL_MAXS || (nself && n > MSIM_MAX_MINERS) || id_quirk ||
+                     n > msim::WIDE_MAX_M || getenv("MSIM_FORCE_GENERAL") != nullptr;
+    // G holds every miner's explicit chain: one lane of its last window must fit (msim_general_launch.h).
+    if (gen && !msim::gen_fits(n, duration_ms)) return MSIM_E_MINERS;
     const bool sel = nself > 0 && !gen;
     const bool narrow = n <= MSIM_MAX_MINERS && (total_weight == 100 || sel);
     const bool force_wide = getenv("MSIM_FORCE_WIDE") != nullptr && nself == 0;
@@ -710,6 +744,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         c->gh.w.push_back(miners[k].perc);
         c->gh.prop.push_back(miners[k].propagation_ms);
         c->gh.self.push_back(miners[k].is_selfish ? 1 : 0);
+        c->gh.ids.push_back(miners[k].id);
     }
     c->p.duration_ms = duration_ms;
     c->p.m = (int32_t)n;
@@ -719,7 +754,10 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         rho += (double)miners[k].perc / (double)total_weight *
                (miners[k].is_selfish ? 1.0 : 1.0 - exp(-((double)miners[k].propagation_ms + 1.0) / 599999.5));
     c->rho = rho;
-    if (narrow && !force_wide) {
+    if (gen && !narrow) {
+        // G alone: nothing else to prepare (its tables are uploaded on first launch)
+        c->pipe_ok = false;
+    } else if (narrow && !force_wide) {
         for (uint32_t k = 0; k < n; ++k) {
             c->ids[k] = miners[k].id;
             c->perc[k] = miners[k].perc;
@@ -1509,8 +1547,8 @@ const char *msim_strerror(int code)
     case MSIM_OK: return "ok";
     case MSIM_E_INVALID: return "invalid argument";
     case MSIM_E_WEIGHTS: return "miner weights must be integers adding up to the total weight (100 for percentages)";
-    case MSIM_E_SELFISH: return "at most 4 selfish miners, in networks of at most 15 miners, are supported on the device path";
-    case MSIM_E_MINERS: return "too many miners (max 4096; networks with a selfish miner: 15) or duplicate miner ids";
+    case MSIM_E_SELFISH: return "reserved (not returned: every network with selfish miners runs)";
+    case MSIM_E_MINERS: return "network too large for the general engine (one run's explicit chains, miners x blocks per run x 12 B, exceed 8 GiB)";
     case MSIM_E_HIP: return "HIP runtime error";
     case MSIM_E_CAPACITY: return "a run exceeded the compact state capacity";
     case MSIM_E_PICK: return "PickFinder fell through its table";

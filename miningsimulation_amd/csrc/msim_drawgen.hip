@@ -90,11 +90,10 @@ struct DevCtx {
         uint32_t below;
         asm volatile("v_mbcnt_lo_u32_b32 %0, %1, 0\n\tv_mbcnt_hi_u32_b32 %0, %2, %0"
                      : "=&v"(below) : "s"((uint32_t)mask), "s"((uint32_t)(mask >> 32)));
-        const bool mine = s & ((amask >> 0) != 0ull);
         uint32_t base = 0;
-        if (mine & (below == 0u)) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
+        if (s & (below == 0u)) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
         base = __builtin_amdgcn_readlane(base, (uint32_t)(__ffsll((unsigned long long)mask) - 1));
-        if (!mine) return;
+        if (!s) return;
         uint32_t lane;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=&v"(lane));
         if (!((amask >> lane) & 1ull)) return;

@@ -42,14 +42,25 @@ enum : uint32_t {
 // One network (a sweep point). Weights are integers summing to W; W = 100 is the reference's percentages
 // with PERC_MULTIPLIER = UINT64_MAX / 100 (simulation.h:18), any other W is SURVEY Appendix C's
 // generalisation (multiplier UINT64_MAX / W).
+//
+// Miner ids. The reference identifies a block's creator by Miner::id, not by the miner's position: a
+// block is (miner_id, arrival) (simulation.h:22-38), MaybeReorg's walk compares blocks by that pair and
+// counts a popped block as stale when its miner_id is the miner's own id (simulation.h:130-133), and
+// MinerStats counts the best chain's blocks whose miner_id equals the miner's id (main.cpp:24-26), Genesis
+// (id UINT_MAX, simulation.h:31-33) included. So two miners that share an id share their blocks' identity,
+// their stale counting and their found counts. G stores as a block's owner the id's CLASS: the lowest index
+// of a miner with that id (cls[k]); owners are then equal exactly when the reference's ids are, and the
+// per-owner counters of a class hold the blocks of every miner with that id. The class whose id is
+// UINT_MAX (umax, or GEN_GENESIS when no miner has it) also owns Genesis in MinerStats.
 struct GenParams {
     int64_t duration_ms;
     uint64_t mult;         // UINT64_MAX / W
     uint32_t m;            // miners
-    uint32_t pad;
+    uint32_t umax;         // class of id UINT_MAX, or GEN_GENESIS
     const uint64_t *cum;   // [m] cumulative weights
     const int64_t *prop;   // [m] propagation (ms)
     const uint8_t *self;   // [m] 1: selfish (simulation.h:55)
+    const uint32_t *cls;   // [m] id class: lowest index with the same Miner::id
 };
 
 // PickFinder (simulation.h:213-221): the first miner k whose cumulative weight * mult exceeds u. With
@@ -83,7 +94,8 @@ struct Gen {
     St &st;
     const GenParams &g;
     uint32_t base;   // absolute height of window index 0
-    uint32_t bcs;    // best_chain_size of the previous event (main.cpp:149, 171), window-relative
+    int32_t bcs;     // best_chain_size of the previous event (main.cpp:149, 171), window-relative; negative
+                     // when a fold took blocks that arrived after that event (one miner, zero delays)
     int64_t now;     // the current time (a fold only takes blocks that arrived by now)
     uint32_t err;
 
@@ -116,7 +128,7 @@ struct Gen {
             st.set_size(k, n - s);
         }
         base += s;
-        bcs -= s;
+        bcs -= (int32_t)s;
         return s;
     }
 
@@ -145,13 +157,13 @@ struct Gen {
         if (g.self[k]) {
             const uint32_t n = st.size(k);
             const bool one = n >= 1 && st.arr(k, n - 1) == GEN_SELFISH && (n < 2 || st.arr(k, n - 2) != GEN_SELFISH);
-            if (one && bcs == n) {
+            if (one && bcs == (int32_t)n) {
                 st.set_arr(k, n - 1, t + p);
-                return push(k, k, t + p);
+                return push(k, g.cls[k], t + p);
             }
-            return push(k, k, GEN_SELFISH);
+            return push(k, g.cls[k], GEN_SELFISH);
         }
-        return push(k, k, t + p);
+        return push(k, g.cls[k], t + p);
     }
 
     // simulation.h:118-121 PublishedChain length: the chain minus UnpublishedBlocks(t) (simulation.h:79-89).
@@ -214,7 +226,7 @@ struct Gen {
         for (uint32_t i = n; i > 0; --i) {
             const uint32_t o = st.own(k, n - 1);
             if (o == st.own((uint32_t)bk, i - 1) && st.arr(k, n - 1) == st.arr((uint32_t)bk, i - 1)) break;
-            if (o == k) st.add_stale(k);
+            if (o == g.cls[k]) st.add_stale(k);  // chain.back().miner_id == id
             --n;
         }
         if (bl > st.cap) {
@@ -269,7 +281,7 @@ struct Gen {
                 reorg(k, bk, bl);
             }
             if (err) break;
-            bcs = bl;  // main.cpp:171
+            bcs = (int32_t)bl;  // main.cpp:171
             bool have = false;  // main.cpp:176-182 EarliestArrival
             int64_t ea = 0;
             for (uint32_t k = 0; k < g.m; ++k) {
@@ -289,21 +301,28 @@ struct Gen {
         return true;
     }
 
-    // main.cpp:22-26: blocks of miner k in the final best chain (folded prefix + window).
+    // main.cpp:22-26: blocks of miner k in the final best chain (folded prefix + window): the blocks of
+    // its id class, plus Genesis when its id is UINT_MAX.
     MSIM_HD uint32_t found(uint32_t k, const GenOut &o) const
     {
-        uint32_t f = st.pre(k);
-        for (uint32_t i = 0; i < o.best_len; ++i) f += st.own((uint32_t)o.best, i) == k ? 1u : 0u;
+        const uint32_t c = g.cls[k];
+        uint32_t f = st.pre(c) + (c == g.umax ? 1u : 0u);
+        for (uint32_t i = 0; i < o.best_len; ++i) f += st.own((uint32_t)o.best, i) == c ? 1u : 0u;
         return f;
     }
     // The same for every miner in one pass: the window of the final best chain is added to `pre`, which
-    // then holds every miner's blocks_found.
+    // then holds every id class's blocks (found_after_count gives a miner's blocks_found).
     MSIM_HD void count_best(const GenOut &o)
     {
         for (uint32_t i = 0; i < o.best_len; ++i) {
             const uint32_t ow = st.own((uint32_t)o.best, i);
             if (ow != GEN_GENESIS) st.add_pre(ow, 1u);
         }
+    }
+    MSIM_HD uint32_t found_after_count(uint32_t k) const
+    {
+        const uint32_t c = g.cls[k];
+        return st.pre(c) + (c == g.umax ? 1u : 0u);
     }
     // the best chain's length minus Genesis (main.cpp:28's best_chain.size() - 1)
     MSIM_HD static uint32_t best_height(const GenOut &o) { return o.base + o.best_len - 1u; }

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void msim_gen_kernel(const GenArgs a)
         const size_t gi = (size_t)point * a.rpp + rel;
         unsigned long long *sums = (unsigned long long *)(a.sums + (size_t)point * 6 * a.max_m);
         for (uint32_t k = 0; k < g.m; ++k) {
-            const uint32_t f = s.pre(k), st = s.stale(k);
+            const uint32_t f = e.found_after_count(k), st = s.stale(k);
             if (a.records) {
                 a.records[2 * (gi * g.m + k) + 0] = f;
                 a.records[2 * (gi * g.m + k) + 1] = st;

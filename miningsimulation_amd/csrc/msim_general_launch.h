@@ -47,24 +47,33 @@ struct GenTier {
 
 // Window tiers for networks of up to max_m miners and runs of up to max_duration ms: 256 blocks (every
 // honest or minority-selfish run folds well inside it), 4 096, and the largest chain a run can have (a
-// selfish miner that never reveals: every block, mu + 10 sigma + 64). Lanes per tier fill `budget` bytes.
-inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTier (&t)[3])
+// selfish miner that never reveals: every block, mu + 10 sigma + 64). Lanes per tier fill `budget` bytes:
+// whole waves while a wave fits, down to ONE lane for a window too large for a wave (the last tier of a
+// large network: a run only reaches it with a selfish majority, and a lane serves its list in turn).
+constexpr double GEN_MAX_LANE_BYTES = 8.0 * 1024 * 1024 * 1024;  // one lane's chains: larger networks are rejected
+inline double gen_lane_bytes(uint32_t max_m, uint32_t cap) { return (double)max_m * (cap * 12.0 + 12.0); }
+inline uint32_t gen_last_cap(int64_t max_duration)
 {
     const double mu = (double)max_duration / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
     uint64_t top = (uint64_t)ceil(mu + 10.0 * sd + 64.0) + 2;
     top = (top + 255) / 256 * 256;
-    const uint32_t caps[3] = {256u, 4096u, (uint32_t)(top > 4096 ? top : 4096)};
+    return (uint32_t)(top > 4096 ? top : 4096);
+}
+inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTier (&t)[3])
+{
+    const uint32_t caps[3] = {256u, 4096u, gen_last_cap(max_duration)};
     const int nt = caps[2] > 4096u ? 3 : 2;
     for (int i = 0; i < nt; ++i) {
-        const double per_lane = (double)max_m * (caps[i] * 12.0 + 12.0);
-        double l = floor(budget / per_lane / 256.0) * 256.0;
-        if (l < 256.0) l = 256.0;
+        double l = floor(budget / gen_lane_bytes(max_m, caps[i]));
+        l = l >= 64.0 ? floor(l / 64.0) * 64.0 : (l >= 1.0 ? l : 1.0);
         if (l > 65536.0) l = 65536.0;
         t[i].cap = caps[i];
         t[i].lanes = (size_t)l;
     }
     return nt;
 }
+// Whether G can hold a network of m miners and runs of duration_ms (one lane of its last window).
+inline bool gen_fits(uint32_t m, int64_t duration_ms) { return gen_lane_bytes(m, gen_last_cap(duration_ms)) <= GEN_MAX_LANE_BYTES; }
 
 // Workspace of G: the tier lists and the largest tier's chains and counters.
 struct GenWs {

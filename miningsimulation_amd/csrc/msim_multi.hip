@@ -6,11 +6,14 @@
 // so here the run range is cut into contiguous shards, one per device; each device runs its shard
 // through msim_launch (device-resident, asynchronous on its own stream), and the per-miner msim_sums (integers)
 // are combined by ONE ncclAllReduce over a single-process communicator (ncclCommInitAll: RCCL over xGMI
-// on MI355X). Integer sums make the result bit-identical to msim_run for every device count.
+// on MI355X), cached per device list. Integer sums make the result bit-identical to msim_run for every
+// device count.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/msim.h"
@@ -116,6 +119,48 @@ void enqueue_shard(const Job &job, uint32_t seed_base, Shard &sh)
     }
 }
 
+// Single-process communicators, one per device list, created on first use and kept for the life of the
+// process (ncclCommInitAll costs milliseconds to seconds per call; a host driver that calls msim_run_multi
+// once per sweep point must not pay it every time). A communicator is used by one call at a time: its
+// entry's mutex is held from the first enqueue to the last synchronisation. An entry whose collectives
+// failed is dropped (destroyed) so that the next call starts from a fresh communicator.
+struct CommEntry {
+    std::vector<int> devs;
+    std::vector<ncclComm_t> comms;
+    std::mutex use;
+};
+std::mutex g_comm_mu;
+std::vector<std::shared_ptr<CommEntry>> g_comms;
+
+std::shared_ptr<CommEntry> comm_for(const std::vector<int> &devs, int *rc)
+{
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    for (const auto &e : g_comms)
+        if (e->devs == devs) return e;
+    auto e = std::make_shared<CommEntry>();
+    e->devs = devs;
+    e->comms.assign(devs.size(), nullptr);
+    if (ncclCommInitAll(e->comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
+        *rc = MSIM_E_HIP;
+        return nullptr;
+    }
+    g_comms.push_back(e);
+    return e;
+}
+
+void comm_drop(const std::shared_ptr<CommEntry> &e)
+{
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    for (size_t i = 0; i < g_comms.size(); ++i)
+        if (g_comms[i] == e) {
+            for (ncclComm_t c : e->comms)
+                if (c) (void)ncclCommDestroy(c);
+            e->comms.assign(e->comms.size(), nullptr);
+            g_comms.erase(g_comms.begin() + (long)i);
+            return;
+        }
+}
+
 // Shards [run_begin, run_begin + n_runs) over the devices, runs them, all-reduces; acc = reduced sums.
 // Every buffer of every device is allocated before anything is enqueued, and the collectives are issued
 // for all devices by this one thread inside one ncclGroupStart / ncclGroupEnd (the single-process
@@ -140,27 +185,35 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
         sh[g].n = base + (g < rem ? 1 : 0);
         if (rc == MSIM_OK) rc = alloc_shard(job, sh[g]);
     }
-    std::vector<ncclComm_t> comms(n_devices, nullptr);
-    if (rc == MSIM_OK && ncclCommInitAll(comms.data(), (int)n_devices, devs.data()) != ncclSuccess) {
-        rc = MSIM_E_HIP;
-        comms.assign(n_devices, nullptr);
-    }
+    // one device: its sums are the result (no collective)
+    std::shared_ptr<CommEntry> ce;
+    if (rc == MSIM_OK && n_devices > 1) ce = comm_for(devs, &rc);
+    std::unique_lock<std::mutex> use;
+    if (ce) use = std::unique_lock<std::mutex>(ce->use);
     if (rc == MSIM_OK) {
         for (auto &x : sh) enqueue_shard(job, seed_base, x);
-        if (ncclGroupStart() != ncclSuccess) {
+        bool coll_failed = false;
+        if (ce && ncclGroupStart() != ncclSuccess) {
             rc = MSIM_E_HIP;
-        } else {
+            coll_failed = true;
+        } else if (ce) {
             for (uint32_t g = 0; g < n_devices; ++g)
-                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv, ncclUint64, ncclSum, comms[g], sh[g].s) != ncclSuccess ||
-                    ncclAllReduce(sh[g].d_stat, sh[g].d_stat, 2, ncclUint32, ncclSum, comms[g], sh[g].s) != ncclSuccess)
+                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv, ncclUint64, ncclSum, ce->comms[g], sh[g].s) != ncclSuccess ||
+                    ncclAllReduce(sh[g].d_stat, sh[g].d_stat, 2, ncclUint32, ncclSum, ce->comms[g], sh[g].s) != ncclSuccess)
                     rc = MSIM_E_HIP;
             if (ncclGroupEnd() != ncclSuccess) rc = MSIM_E_HIP;
+            coll_failed = rc != MSIM_OK;
         }
         for (auto &x : sh)
             if (hipSetDevice(x.device) != hipSuccess || hipStreamSynchronize(x.s) != hipSuccess) rc = rc ? rc : MSIM_E_HIP;
         for (const auto &x : sh)
             if (x.rc) rc = rc ? rc : x.rc;
+        if (coll_failed) {
+            if (use.owns_lock()) use.unlock();
+            comm_drop(ce);
+        }
     }
+    if (use.owns_lock()) use.unlock();
     acc.assign(job.nv, 0);
     uint32_t st[2] = {0, 0};
     if (rc == MSIM_OK) {  // every device holds the reduced sums: read the first one's
@@ -171,10 +224,7 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
         else if (st[1] != 0)
             rc = MSIM_E_CAPACITY;
     }
-    for (uint32_t g = 0; g < n_devices; ++g) {
-        free_shard(sh[g]);
-        if (comms[g]) (void)ncclCommDestroy(comms[g]);
-    }
+    for (uint32_t g = 0; g < n_devices; ++g) free_shard(sh[g]);
     return rc;
 }
 

@@ -87,7 +87,10 @@ def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=No
     # Everything that touches the launch's outputs runs on the launch stream: the adds read `part` / `pst`
     # after the kernels that wrote them, the next chunk's launch overwrites them only after the adds, and
     # the all-reduce (RCCL enqueues on the current stream) sees the final sums.
+    # The buffers above were zeroed on the caller's current stream: the launch stream waits for that first.
     ctx = torch.cuda.stream(stream) if (stream is not None and dev.type == "cuda") else contextlib.nullcontext()
+    if stream is not None and dev.type == "cuda":
+        stream.wait_stream(torch.cuda.current_stream(dev))
     with ctx:
         for off in range(0, n, max(chunk, 1)):
             cn = min(chunk, n - off)

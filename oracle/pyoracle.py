@@ -111,14 +111,15 @@ def run(percs, props, selfish, duration_ms: int, seed_interval: int, seed_picker
 
 
 def run_batch(percs, props, selfish, duration_ms: int, n_runs: int, run_begin: int = 0, seed_base: int = 1000,
-              threads: int = 8, total_weight: int = 100):
+              threads: int = 8, total_weight: int = 100, ids: Optional[Sequence[int]] = None):
     """Per-run stats for runs [run_begin, run_begin+n) with the SURVEY seed convention.
 
     total_weight != 100: `percs` are integer weights summing to it (SURVEY Appendix C generalisation).
+    ids: Miner::id per miner (default: the index).
     Returns (found [n, M] int64, stale [n, M] int64, share [n, M] f64, rate [n, M] f64)."""
     m = len(percs)
     out = (ORunStats * (n_runs * m))()
-    rc = lib().oracle_run_batch_w(_miners(percs, props, selfish), m, duration_ms, total_weight, run_begin, n_runs,
+    rc = lib().oracle_run_batch_w(_miners(percs, props, selfish, ids), m, duration_ms, total_weight, run_begin, n_runs,
                                   seed_base & 0xFFFFFFFF, threads, out, None)
     if rc:
         raise RuntimeError(f"oracle_run_batch rc={rc}")

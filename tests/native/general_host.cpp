@@ -42,21 +42,37 @@ extern "C" {
 
 // One run with seeds (si, sp); weights sum to W. Returns the error bits (GERR_*); on success fills
 // found / stale [m] and the best chain height (length - 1).
-uint32_t gen_run(const uint64_t *weights, const int64_t *props, const uint8_t *selfish, int m, uint64_t W,
-                 int64_t duration, uint32_t si, uint32_t sp, uint32_t cap, uint32_t *found, uint32_t *stale,
-                 uint32_t *best_height, uint32_t *base)
+// ids: Miner::id per miner (NULL: the index); the id classes are built as the library's host code does
+// (msim_api.hip gen_id_classes: the lowest index with the same id; the class of id UINT_MAX owns Genesis).
+uint32_t gen_run(const uint64_t *weights, const int64_t *props, const uint8_t *selfish, const uint32_t *ids, int m,
+                 uint64_t W, int64_t duration, uint32_t si, uint32_t sp, uint32_t cap, uint32_t *found,
+                 uint32_t *stale, uint32_t *best_height, uint32_t *base)
 {
     std::vector<uint64_t> cum(m);
+    std::vector<uint32_t> cls(m);
     uint64_t c = 0;
-    for (int k = 0; k < m; ++k) cum[k] = (c += weights[k]);
+    uint32_t umax = GEN_GENESIS;
+    for (int k = 0; k < m; ++k) {
+        cum[k] = (c += weights[k]);
+        const uint32_t id = ids ? ids[k] : (uint32_t)k;
+        cls[k] = (uint32_t)k;
+        for (int j = 0; j < k; ++j)
+            if ((ids ? ids[j] : (uint32_t)j) == id) {
+                cls[k] = (uint32_t)j;
+                break;
+            }
+        if (id == 0xFFFFFFFFu) umax = cls[k];
+    }
     GenParams g;
     memset(&g, 0, sizeof(g));
     g.duration_ms = duration;
     g.mult = 0xFFFFFFFFFFFFFFFFull / W;
     g.m = (uint32_t)m;
+    g.umax = umax;
     g.cum = cum.data();
     g.prop = props;
     g.self = selfish;
+    g.cls = cls.data();
     HostStore s((uint32_t)m, cap);
     Gen<HostStore> e(s, g);
     GenOut o;

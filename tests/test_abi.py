@@ -45,8 +45,8 @@ def test_config_validation_without_gpu(msim_lib_path):
     bad = [
         ([Miner(0, 60, 1000), Miner(1, 30, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 90
         ([Miner(0, 60, 1000), Miner(1, 50, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 110
-        ([Miner(0, 50, 1000), Miner(0, 50, 1000)], _lib.MSIM_E_MINERS),             # duplicate id
-        ([Miner(k, 1 if k < 100 else 0, 1000) for k in range(4097)], _lib.MSIM_E_MINERS),
+        # one run's explicit chains above 8 GiB on the general engine (20 000 miners x ~55 k blocks)
+        ([Miner(k, 1 if k < 100 else 0, 1000) for k in range(20000)], _lib.MSIM_E_MINERS),
         ([Miner(0, 50, -1), Miner(1, 50, 1000)], _lib.MSIM_E_INVALID),
     ]
     for miners, code in bad:
@@ -68,6 +68,20 @@ def test_config_validation_without_gpu(msim_lib_path):
                       ([Miner(k, 7 if k < 10 else 5, 1000, k == 0) for k in range(16)], 100),
                       ([Miner(k, 1, 1000, k == 0) for k in range(16)], 16)):
         assert Simulation(miners, total_weight=W).pipeline_info(1024)["uses_pipeline"] == 4
+    # the reference's id semantics (shared / Genesis ids, simulation.h:31-38, main.cpp:24-26) and honest
+    # networks beyond the large-network pipeline run on the general engine too
+    for miners in ([Miner(0, 50, 1000), Miner(0, 50, 1000)],
+                   [Miner(0xFFFFFFFF, 30, 1000)] + [Miner(k, 10, 1000) for k in range(7)],
+                   [Miner(k, 1 if k < 100 else 0, 1000) for k in range(4097)]):
+        sim = Simulation(miners)
+        assert sim.pipeline_info(1024)["uses_pipeline"] == 4
+    # G's windows follow its byte budget (one lane of the last window at least): a 1 026-miner network with a
+    # selfish miner, and the fallback G reserves behind every entity-engine launch, stay bounded
+    big = Simulation([Miner(k, w, 1000, k == 0) for k, w in enumerate([30720, 29696] + [41] * 1024)],
+                     total_weight=102400)
+    assert big.pipeline_info(1024)["uses_pipeline"] == 4
+    assert big.workspace_bytes(65536) < 3 * 2**30, big.workspace_bytes(65536)
+    assert Simulation(setup_miners(1000, selfish_perc=40)).workspace_bytes(131072) < 2**30
     # the large-network path (msim_wide.h): more than 15 honest miners, or integer weights
     assert Simulation([Miner(k, 7 if k < 10 else 5, 1000) for k in range(16)]).wide
     assert not Simulation(setup_miners()).wide

@@ -35,3 +35,27 @@ def test_single_rank_unchanged():
     d = _bench("--gpus", "1", "--steps", "2", "--warmup", "0")
     assert d["n_gpus"] == 1
     assert "cpu_baseline" not in d
+
+
+def test_spawn_eight_ranks():
+    """The driver's 8-GPU node: eight ranks, one JSON line, the aggregate over all of them."""
+    d = _bench("--gpus", "8", "--steps", "2", "--warmup", "1")
+    assert d["n_gpus"] == 8
+    assert abs(d["value"] * d["ms_per_step"] * 2 / 1e3 - 8 * 2 * 32768) < 1e-3 * 8 * 2 * 32768
+
+
+def test_spawn_failing_rank_ends_job():
+    """A rank that dies (here: rank 1 of 4, before its collectives) ends the job quickly with a non-zero exit
+    and no JSON line, instead of leaving rank 0 waiting in a collective."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MSIM_BENCH_STUB_FAIL_RANK"] = "1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub", "--no-cpu-baseline", "--gpus", "4",
+                        "--steps", "2", "--warmup", "0"], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=ROOT)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "rank 1 exited" in r.stderr, r.stderr[-2000:]
+    assert time.monotonic() - t0 < 120

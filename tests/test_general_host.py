@@ -21,20 +21,22 @@ def gen(native_tests):
     lib = ctypes.CDLL(native_tests["general_host"])
     lib.gen_run.restype = ctypes.c_uint32
     lib.gen_run.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
-                            ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_uint64, ctypes.c_int64,
+                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                            ctypes.c_uint64, ctypes.c_int64,
                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                             ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                             ctypes.POINTER(ctypes.c_uint32)]
 
-    def run(weights, props, selfish, duration, si, sp, cap, W=100):
+    def run(weights, props, selfish, duration, si, sp, cap, W=100, ids=None):
         m = len(weights)
         f = (ctypes.c_uint32 * m)()
         s = (ctypes.c_uint32 * m)()
         bh = ctypes.c_uint32()
         base = ctypes.c_uint32()
+        idp = (ctypes.c_uint32 * m)(*ids) if ids is not None else None
         err = lib.gen_run((ctypes.c_uint64 * m)(*weights), (ctypes.c_int64 * m)(*props),
-                          (ctypes.c_uint8 * m)(*[1 if x else 0 for x in selfish]), m, W, duration, si, sp, cap, f, s,
-                          ctypes.byref(bh), ctypes.byref(base))
+                          (ctypes.c_uint8 * m)(*[1 if x else 0 for x in selfish]), idp, m, W, duration, si, sp, cap,
+                          f, s, ctypes.byref(bh), ctypes.byref(base))
         return err, np.array([[f[k], s[k]] for k in range(m)], dtype=np.int64), bh.value, base.value
 
     return run
@@ -46,19 +48,22 @@ def _rand_weights(m, rng, total=100):
     return [b[i + 1] - b[i] for i in range(m)]
 
 
-def _check_batch(gen, oracle, weights, props, selfish, duration, n_runs, seed_base, cap, W=100, allow_cap=False):
+def _check_batch(gen, oracle, weights, props, selfish, duration, n_runs, seed_base, cap, W=100, allow_cap=False,
+                 ids=None):
     """Runs 0..n-1 with the SURVEY seed convention (base + 2r, base + 2r + 1) vs the oracle's batch."""
-    f, s, _, _ = oracle.run_batch(weights, props, selfish, duration, n_runs, 0, seed_base, threads=8, total_weight=W)
+    f, s, _, _ = oracle.run_batch(weights, props, selfish, duration, n_runs, 0, seed_base, threads=8, total_weight=W,
+                                  ids=ids)
     folded = checked = 0
     for r in range(n_runs):
         si, sp = (seed_base + 2 * r) & 0xFFFFFFFF, (seed_base + 2 * r + 1) & 0xFFFFFFFF
-        err, res, bh, base = gen(weights, props, selfish, duration, si, sp, cap, W)
+        err, res, bh, base = gen(weights, props, selfish, duration, si, sp, cap, W, ids)
         if err == GERR_CAP and allow_cap:
             continue
         assert err == 0, (err, weights, props, selfish, duration, r)
         exp = np.stack([f[r], s[r]], axis=1)
         assert np.array_equal(exp, res), (weights, props, selfish, duration, r, exp.tolist(), res.tolist())
-        assert bh == int(f[r].sum()), (bh, int(f[r].sum()))
+        if ids is None:
+            assert bh == int(f[r].sum()), (bh, int(f[r].sum()))
         folded += base > 0
         checked += 1
     return folded, checked
@@ -115,3 +120,39 @@ def test_zero_duration_and_zero_delay(gen, oracle):
     _check_batch(gen, oracle, [50, 30, 20], [0, 0, 0], [False, True, False], 0, 2, 3, cap=64)
     _check_batch(gen, oracle, [50, 30, 20], [0, 0, 0], [False, True, False], 10 * DAY, 3, 3, cap=64)
     _check_batch(gen, oracle, [100], [0], [True], 3 * DAY, 2, 11, cap=4096)
+
+
+def test_shared_ids(gen, oracle):
+    """Miners sharing an id share their blocks' identity (simulation.h:35-38), each other's stale counting
+    (simulation.h:133) and found counts (main.cpp:24-26): the reference's values, not a rejection."""
+    # two honest miners with id 3 and one selfish miner sharing id 3 with them; equal delays make equal
+    # (id, arrival) blocks of different miners possible, and short windows force folds
+    for props in ([1000] * 5, [0] * 5, [100, 100, 2000, 2000, 100]):
+        _check_batch(gen, oracle, [30, 25, 20, 15, 10], props, [False] * 5, 30 * DAY, 6, 31, cap=64,
+                     ids=[3, 3, 7, 3, 9])
+        _check_batch(gen, oracle, [30, 25, 20, 15, 10], props, [True, False, False, False, False], 30 * DAY, 6, 77,
+                     cap=4096, ids=[3, 3, 7, 3, 9])
+    # every miner with one id
+    _check_batch(gen, oracle, [40, 35, 25], [500] * 3, [False, True, False], 10 * DAY, 4, 5, cap=128, ids=[1, 1, 1])
+
+
+def test_genesis_id(gen, oracle):
+    """A miner whose id is UINT_MAX is Genesis's namesake (simulation.h:31-33): MinerStats counts Genesis
+    among its blocks (main.cpp:24-26)."""
+    U = 0xFFFFFFFF
+    for ids in ([U, 1, 2, 3], [0, U, 2, U], [U, U, U, U]):
+        _check_batch(gen, oracle, [40, 30, 20, 10], [1000] * 4, [False] * 4, 7 * DAY, 4, 123, cap=64, ids=ids)
+        _check_batch(gen, oracle, [40, 30, 20, 10], [1000] * 4, [True, False, False, False], 7 * DAY, 4, 9, cap=4096,
+                     ids=ids)
+    # zero-duration run: the best chain is Genesis alone; the UINT_MAX miner has found one block
+    f, _, _, _ = oracle.run_batch([50, 50], [0, 0], [False, False], 0, 1, 0, 1, ids=[U, 0])
+    assert f[0].tolist() == [1, 0]
+    _check_batch(gen, oracle, [50, 50], [0, 0], [False, False], 0, 2, 1, cap=64, ids=[U, 0])
+
+
+def test_single_miner_zero_delay_fold(gen, oracle):
+    """One miner, zero delay, tiny window: folds take blocks that arrived after the previous event's best
+    chain was recorded (the window-relative best_chain_size goes below zero); ADVICE r3."""
+    _check_batch(gen, oracle, [100], [0], [False], 10 * DAY, 4, 17, cap=16)
+    # a lone selfish miner never publishes (its lead never drops), so nothing folds: the window holds the run
+    _check_batch(gen, oracle, [100], [0], [True], 10 * DAY, 4, 17, cap=4096)

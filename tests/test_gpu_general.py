@@ -34,16 +34,23 @@ def _rand_weights(m, rng, total=100):
     return [b[i + 1] - b[i] for i in range(m)]
 
 
-def _vs_oracle(msim, oracle, p, q, s, n, seed, dur, W=100, path=None):
-    miners = [msim.Miner(k, p[k], q[k], bool(s[k])) for k in range(len(p))]
+def _vs_oracle(msim, oracle, p, q, s, n, seed, dur, W=100, path=None, ids=None):
+    ids = list(range(len(p))) if ids is None else ids
+    miners = [msim.Miner(ids[k], p[k], q[k], bool(s[k])) for k in range(len(p))]
     sim = msim.Simulation(miners, dur, total_weight=W)
     if path is not None:
         assert sim.pipeline_info(n)["uses_pipeline"] == path
     res = sim.run(n, 0, seed, 0, per_run=True)
-    f, st, _, _ = oracle.run_batch(p, q, s, dur, n, 0, seed, threads=16, total_weight=W)
+    f, st, sh, rt = oracle.run_batch(p, q, s, dur, n, 0, seed, threads=16, total_weight=W, ids=ids)
     assert np.array_equal(res.found.astype(np.int64), f), (p, q, s, dur, seed)
     assert np.array_equal(res.stale.astype(np.int64), st), (p, q, s, dur, seed)
-    assert np.array_equal(res.best_height.astype(np.int64), f.sum(axis=1))
+    if len(set(ids)) == len(ids) and 0xFFFFFFFF not in ids:
+        assert np.array_equal(res.best_height.astype(np.int64), f.sum(axis=1))
+    # MinerStats summed in run order (main.cpp:211-217): the exact f64 aggregate
+    for k in range(len(p)):
+        assert res.stats_total[k].blocks_found == int(f[:, k].sum())
+        assert res.stats_total[k].blocks_share == sum(sh[:, k].tolist())
+        assert res.stats_total[k].stale_rate == sum(rt[:, k].tolist())
     return res
 
 
@@ -115,3 +122,31 @@ def test_gpu_general_sweep(msim, oracle):
         f, st, _, _ = oracle.run_batch(p, q, s, 30 * DAY, 32, 0, 500, threads=16)
         assert np.array_equal(res[i].found.astype(np.int64), f), i
         assert np.array_equal(res[i].stale.astype(np.int64), st), i
+
+
+def test_gpu_general_large_honest_network(msim, oracle):
+    """5 000 honest miners (more than the large-network pipeline's 4 096): G, per run vs the oracle."""
+    rng = random.Random(11)
+    p = [2000, 1500] + [rng.randint(1, 3) for _ in range(4998)]
+    W = sum(p)
+    _vs_oracle(msim, oracle, p, [1000] * 5000, [False] * 5000, 32, 321, DAY, W=W, path=4)
+
+
+def test_gpu_general_shared_ids(msim, oracle):
+    """Miners sharing an id (the reference accepts them): shared block identity (simulation.h:35-38), stale
+    counting (simulation.h:133) and found counts (main.cpp:24-26), bit-exact per run, on G."""
+    _vs_oracle(msim, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [False] * 9, 64, 1000, 30 * DAY,
+               path=4, ids=[0, 1, 2, 0, 4, 5, 1, 7, 0])
+    _vs_oracle(msim, oracle, [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, 64, 99, 30 * DAY,
+               path=4, ids=[5, 5, 2, 3, 4, 5, 6, 7, 8])
+    _vs_oracle(msim, oracle, [34, 33, 33], [0, 0, 0], [False] * 3, 32, 7, 7 * DAY, path=4, ids=[9, 9, 9])
+
+
+def test_gpu_general_genesis_id(msim, oracle):
+    """A miner with id UINT_MAX (Genesis's id, simulation.h:31-33) counts Genesis among its found blocks."""
+    U = 0xFFFFFFFF
+    _vs_oracle(msim, oracle, [30, 29, 12, 11, 8, 5, 3, 1, 1], [100] * 9, [False] * 9, 64, 1000, 30 * DAY,
+               path=4, ids=[U, 1, 2, 3, 4, 5, 6, 7, 8])
+    _vs_oracle(msim, oracle, [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [True] + [False] * 8, 64, 5, 30 * DAY,
+               path=4, ids=[0, 1, 2, 3, 4, 5, 6, 7, U])
+    _vs_oracle(msim, oracle, [60, 40], [10, 10], [False, False], 8, 3, 0, path=4, ids=[U, U])
