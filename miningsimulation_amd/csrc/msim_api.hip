@@ -6,6 +6,7 @@
 // one run per lane, and the per-miner sums are reduced on the device in integers.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -105,7 +106,6 @@ struct msim_sweep {
     };
     std::vector<Group> groups;
     std::vector<std::pair<int, void *>> sdev;  // (device, SelParams[n_points] + point lists)
-    const msim_config *tab_cfg = nullptr;      // config whose log / jump tables the draws use
     // General-engine view of every point (G finishes what E2 cannot; a sweep with a general point runs on G)
     bool general = false;
     std::vector<GenHost> gens;
@@ -335,33 +335,14 @@ int wide_tables(msim_config *c, msim::WideArgs *a)
 }
 
 // ---------------------------------------------------------------- entity-engine path (msim_sel_launch.h)
-constexpr double SEL_SLICE_BUDGET = 32.0 * (1ull << 30);  // word stream per slice (bytes)
-
-uint32_t word_draw_slots()
-{
-    int dev = 0, cus = 0, blocks = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        msim::word_draws_blocks_per_cu(&blocks) != hipSuccess || cus <= 0 || blocks <= 0)
-        return 8192;
-    return (uint32_t)(cus * blocks * 4);
-}
-
-// E1 draws in-lane by default (SelFastDraw), for a single network and for sweeps alike: on MI355X the
-// configs[3] grid (360 points x 8192 runs) ran 2.92 s in-lane vs 3.63 s reading D1's shared word stream
-// (profiles/r03/sweep_b_*.txt). MSIM_SEL_WORDS=1 restores the word stream (A/B measurements).
-bool sel_use_words(uint32_t np)
-{
-    (void)np;
-    if (const char *e = getenv("MSIM_SEL_WORDS")) return atoi(e) != 0;
-    return false;
-}
-
+// E1 draws in-lane (SelFastDraw) for a single network and for sweeps alike; round 2's shared per-block word
+// stream (D1) is gone: on MI355X the configs[3] grid (360 points x 8192 runs) ran 2.92 s in-lane vs 3.63 s
+// reading the word stream (profiles/r03/sweep_b_*.txt).
 struct SelWs {
-    bool words;
-    msim::SelLayout L;
+    uint32_t nr;  // runs per slice (per point)
     uint32_t wpp, err_cap;
     size_t cold_lanes;
-    size_t counts_off, partials_off, retry_off, list_off, cold_off, words_off, gen_off, total;
+    size_t counts_off, partials_off, retry_off, list_off, cold_off, gen_off, total;
     msim::GenWs g;  // G, for the runs E2 cannot finish
 };
 
@@ -374,15 +355,9 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     SelWs w;
-    w.words = sel_use_words(np);
-    if (w.words) {
-        w.L = msim::sel_layout_for(duration_ms, rpp, SEL_SLICE_BUDGET, word_draw_slots());
-    } else {  // one slice of every run (up to 2^22 runs: cold slots ~1.4 GiB), no words
-        w.L = msim::sel_layout_for(duration_ms, 256, SEL_SLICE_BUDGET, 1);
-        const uint64_t want = (rpp + 255) / 256 * 256;
-        w.L.nr = (uint32_t)(want < (1ull << 22) ? want : (1ull << 22));
-        w.L.words_bytes = 0;
-    }
+    // one slice of every run (up to 2^22 runs per point: cold slots ~1.4 GiB)
+    const uint64_t want = (rpp + 255) / 256 * 256;
+    w.nr = (uint32_t)(want < (1ull << 22) ? want : (1ull << 22));
     w.wpp = (uint32_t)((rpp + msim::TPB - 1) / msim::TPB);
     w.err_cap = (uint32_t)(rpp * np);  // every lane can be retried: the list never overflows
     const size_t nv = 6 * (size_t)m;
@@ -392,11 +367,10 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
     w.list_off = al(w.retry_off + (size_t)np * nv * 8);
     // cold slots: one set per E1 lane of a slice (every point x the slice's runs, rounded to whole
     // workgroups) and per E2 lane
-    const size_t e1 = (size_t)np * ((w.L.nr + msim::TPB - 1) / msim::TPB) * msim::TPB;
+    const size_t e1 = (size_t)np * ((w.nr + msim::TPB - 1) / msim::TPB) * msim::TPB;
     w.cold_lanes = e1 > w.err_cap ? e1 : (size_t)w.err_cap;
     w.cold_off = al(w.list_off + (size_t)w.err_cap * 4);
-    w.words_off = al(w.cold_off + w.cold_lanes * msim::SEL_NC * sizeof(msim::ColdAct));
-    w.gen_off = al(w.words_off + w.L.words_bytes);
+    w.gen_off = al(w.cold_off + w.cold_lanes * msim::SEL_NC * sizeof(msim::ColdAct));
     w.g = msim::gen_ws_layout(m, duration_ms, w.err_cap, GEN_FALLBACK_BUDGET);
     w.total = al(w.gen_off + w.g.total);
     return w;
@@ -435,6 +409,18 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
     for (uint32_t k = 0; k < n; ++k) pmax = miners[k].propagation_ms > pmax ? miners[k].propagation_ms : pmax;
     sp->xth = pmax <= 2000 ? 16u : (pmax <= 10000 ? 32u : 48u);
     if (const char *e = getenv("MSIM_SEL_XTH")) sp->xth = (uint32_t)atoi(e);  // A/B override
+    // E1's workgroup pool (msim_sel_kernels.hip sel_pool); A/B overrides MSIM_SEL_POOL="q,lmin,iters"
+    sp->pool_q = 32;
+    sp->pool_lmin = 16;
+    sp->pool_iters = 24;
+    if (const char *e = getenv("MSIM_SEL_POOL")) {
+        unsigned q = 0, l = 0, it = 0;
+        if (sscanf(e, "%u,%u,%u", &q, &l, &it) == 3) {
+            sp->pool_q = q;
+            sp->pool_lmin = l;
+            sp->pool_iters = it;
+        }
+    }
 }
 
 struct SelGroupDev {
@@ -443,12 +429,11 @@ struct SelGroupDev {
     uint32_t uni;  // every point of the group has a uniform propagation delay
 };
 
-// The slice loop of one launch: D1 (words) -> E1 per group -> E2 (retries) -> F.
+// The slice loop of one launch: E1 per group -> E2 (retries) -> G (what E2 cannot finish) -> F.
 int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const msim::GenParams *d_gpts,
-                    const std::vector<SelGroupDev> &groups,
-                    const msim::WordArgs &wt, const SelWs &w, char *ws, uint64_t run_begin, uint64_t rpp,
-                    uint32_t seed_base, void *d_sums, void *d_per_run, void *d_best_height, void *d_status, hipStream_t s,
-                    std::vector<hipEvent_t> *draw_events, std::vector<hipEvent_t> *engine_events)
+                    const std::vector<SelGroupDev> &groups, const msim::LogTab *logt, const SelWs &w, char *ws,
+                    uint64_t run_begin, uint64_t rpp, uint32_t seed_base, void *d_sums, void *d_per_run,
+                    void *d_best_height, void *d_status, hipStream_t s, std::vector<hipEvent_t> *engine_events)
 {
     using namespace msim;
     uint32_t *counts = (uint32_t *)(ws + w.counts_off);
@@ -464,10 +449,7 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     a.wpp = w.wpp;
     a.run_begin = run_begin;
     a.seed_base = seed_base;
-    a.nr = w.L.nr;
-    a.nb = w.L.nb;
-    a.words = w.words ? (const uint32_t *)(ws + w.words_off) : nullptr;
-    a.logt = wt.logt;
+    a.logt = logt;
     a.partials = (uint64_t *)(ws + w.partials_off);
     a.retry_sums = retry;
     a.records = (uint32_t *)d_per_run;
@@ -480,12 +462,6 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     a.cold_lanes = w.cold_lanes;
     a.gen_list = gen_first;
     a.force_gen = getenv("MSIM_SEL_FORCE_GEN") != nullptr ? 1u : 0u;
-    WordArgs da = wt;
-    da.seed_base = seed_base;
-    da.nr = w.L.nr;
-    da.seg = w.L.seg;
-    da.nseg = w.L.nseg;
-    da.words = (uint32_t *)(ws + w.words_off);
     auto event = [&](std::vector<hipEvent_t> *v) -> hipEvent_t {
         hipEvent_t e = nullptr;
         if (v && hipEventCreate(&e) == hipSuccess) {
@@ -496,14 +472,8 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     };
     uint32_t max_ns = 1;
     for (const auto &g : groups) max_ns = g.nscls > max_ns ? g.nscls : max_ns;
-    for (uint64_t s0 = 0; s0 < rpp; s0 += w.L.nr) {
-        const uint32_t sn = (uint32_t)((rpp - s0) < w.L.nr ? (rpp - s0) : w.L.nr);
-        da.run_begin = run_begin + s0;
-        if (w.words) {
-            event(draw_events);
-            if (launch_word_draws(da, s) != hipSuccess) return MSIM_E_HIP;
-            event(draw_events);
-        }
+    for (uint64_t s0 = 0; s0 < rpp; s0 += w.nr) {
+        const uint32_t sn = (uint32_t)((rpp - s0) < w.nr ? (rpp - s0) : w.nr);
         a.s0 = (uint32_t)s0;
         a.sn = sn;
         event(engine_events);
@@ -670,23 +640,6 @@ int sel_config_tables(msim_config *c, const msim::SelParams **pts, const uint32_
     }
     *pts = (const msim::SelParams *)d;
     *plist = (const uint32_t *)((const char *)d + pb);
-    return MSIM_OK;
-}
-
-// Word-draw arguments (tables for the slice geometry) of a network with SelParams sp.
-int sel_word_args(msim_config *tabc, const msim::SelParams &sp, const SelWs &w, msim::WordArgs *da)
-{
-    msim::PipeTables t;
-    const int rc = device_tables(tabc, w.L.seg, w.L.nseg, &t);
-    if (rc) return rc;
-    memset(da, 0, sizeof(*da));
-    da->logt = t.logt;
-    da->jump = t.jump;
-    da->mode = sp.W == 100 ? 0u : 1u;
-    da->W = sp.W;
-    da->m = sp.m;
-    da->mult = sp.mult;
-    for (int k = 0; k < msim::MAXM; ++k) da->cum[k] = sp.cum[k];
     return MSIM_OK;
 }
 
@@ -940,8 +893,8 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         const msim::GenParams *gp = nullptr;
         rc = gen_cached(c->mu, c->gtables, {&cfg->gh}, &gp);
         if (rc) return rc;
-        msim::WordArgs da;
-        rc = sel_word_args(c, cfg->sp, w, &da);
+        const msim::LogTab *lt = nullptr;
+        rc = global_log_table(&lt);
         if (rc) return rc;
         std::vector<SelGroupDev> groups{{msim::sel_ns_class(cfg->sp.ns), 1u, plist, cfg->sp.uniform_prop != 0 ? 1u : 0u}};
         Timing &tm = timing();
@@ -959,8 +912,8 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         } else {
             lk.unlock();
         }
-        rc = sel_launch_impl(cfg->n, 1, pts, gp, groups, da, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
-                             d_per_run, d_best_height, d_status, s, on ? &tm.k1 : nullptr, on ? &tm.engine : nullptr);
+        rc = sel_launch_impl(cfg->n, 1, pts, gp, groups, lt, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
+                             d_per_run, d_best_height, d_status, s, on ? &tm.engine : nullptr);
         if (le) (void)hipEventRecord(le, s);
         return rc;
     }
@@ -1188,7 +1141,6 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
                 }
             if (!placed) w->groups.push_back({nc, {i}});
         }
-        w->tab_cfg = cfgs[0];
     }
     *out = w;
     return MSIM_OK;
@@ -1269,12 +1221,12 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
             groups.push_back({gr.nscls, (uint32_t)gr.points.size(), pl, uni});
             pl += gr.points.size();
         }
-        msim::WordArgs da;
-        int rc = sel_word_args(const_cast<msim_config *>(sw->tab_cfg), sm->sps[0], w, &da);
+        const msim::LogTab *lt = nullptr;
+        int rc = global_log_table(&lt);
         if (rc) return rc;
-        return sel_launch_impl(sw->m, np, (const msim::SelParams *)d, gp, groups, da, w, (char *)d_workspace, run_begin,
+        return sel_launch_impl(sw->m, np, (const msim::SelParams *)d, gp, groups, lt, w, (char *)d_workspace, run_begin,
                                runs_per_point, seed_base, d_sums, d_per_run, d_best_height, d_status,
-                               (hipStream_t)stream, nullptr, nullptr);
+                               (hipStream_t)stream, nullptr);
     }
     const SweepLayout l = sweep_layout(sw->m, np, runs_per_point);
     if (workspace_bytes < l.total) return MSIM_E_INVALID;
@@ -1437,10 +1389,10 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     if (cfg->sel) {
         const SelWs w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
         out->uses_pipeline = 3;
-        out->slice_runs = w.L.nr;
-        out->segment_blocks = w.L.seg;
-        out->segments = w.L.nseg;
-        out->blocks_per_run = w.L.nb;
+        out->slice_runs = w.nr;  // E1 draws in-lane: no draw segments
+        out->segment_blocks = 0;
+        out->segments = 0;
+        out->blocks_per_run = 0;
         out->workspace_bytes = w.total;
         return MSIM_OK;
     }

@@ -13,7 +13,6 @@
 #include "msim_jump.h"
 #include "msim_kernels.h"
 #include "msim_pipeline.h"
-#include "msim_sel_launch.h"
 
 namespace msim {
 
@@ -175,62 +174,6 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
 #pragma unroll
     for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = cx.packed(w);
     a.nslow[(size_t)seg * a.nr + r] = s_cnt[K1_NSL][tid];
-}
-
-// D1 (msim_sel_launch.h): every block's packed word for the entity engine. One lane = (run, segment),
-// both streams jumped to draw seg * SEG (msim_jump.h); per block the interval (fast exactly-checked form,
-// msim_fastdraw.h) and the PickFinder code: floor(u / PERC_MULTIPLIER) (one 64x64 high multiply and one
-// compare: it is p1 = floor(100u / 2^64) or p1 + 1), or for weighted networks the finder itself.
-__global__ __launch_bounds__(256) void msim_word_draws_kernel(const WordArgs a)
-{
-    __shared__ LogTab s_log;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&s_log)[i] = ((const double *)a.logt)[i];
-    __syncthreads();
-    const uint32_t r = blockIdx.x * 256 + tid;  // slice-local run (< nr)
-    const uint32_t seg = blockIdx.y;
-    const uint64_t run = a.run_begin + r;
-    Rng ri = rng_seed(seed_interval(a.seed_base, run));
-    Rng rp = rng_seed(seed_picker(a.seed_base, run));
-    if (seg) jump2(reinterpret_cast<const uint4 *>(a.jump) + (size_t)seg * 128, ri, rp);
-    const uint32_t b0 = seg * a.seg;
-    uint4 *out = reinterpret_cast<uint4 *>(a.words) + ((size_t)(b0 / SEL_TILE) * a.nr + r) * (SEL_TILE / 4);
-    const size_t row = (size_t)a.nr * (SEL_TILE / 4);
-    const uint64_t W = a.mode ? (uint64_t)a.W : 100ull;
-    const uint64_t mult = a.mode ? a.mult : PERC_MULTIPLIER;
-    for (uint32_t t = 0; t < a.seg / SEL_TILE; ++t) {
-#pragma unroll 2
-        for (uint32_t j = 0; j < SEL_TILE / 4; ++j) {
-            uint32_t w[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t I = draw_interval(ri, &s_log);
-                const uint64_t u = rng_next(rp);
-                const uint64_t p1 = __umul64hi(u, W);
-                uint32_t code = (uint32_t)(u >= (p1 + 1) * mult ? p1 + 1 : p1);
-                if (a.mode) {
-                    uint32_t f = 0;
-#pragma unroll
-                    for (int k = 0; k < MAXM; ++k) f += ((uint32_t)k < a.m && a.cum[k] <= code) ? 1u : 0u;
-                    code = f;
-                }
-                w[q] = (I << 7) | code;
-            }
-            out[j] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        out += row;
-    }
-}
-
-hipError_t launch_word_draws(const WordArgs &a, hipStream_t s)
-{
-    hipLaunchKernelGGL(msim_word_draws_kernel, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t word_draws_blocks_per_cu(int *blocks)
-{
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_word_draws_kernel, 256, 0);
 }
 
 __global__ void msim_interval_kernel(const LogTab *__restrict__ lt, const uint64_t *__restrict__ u,

@@ -1,18 +1,11 @@
 // msim_sel_launch.h — host/device interface of the entity-engine path (msim_sel.h): networks with
 // selfish miners (BASELINE configs[2], configs[3]).
 //
-//   D1 msim_word_draws_kernel   (run, segment) workers jump both xoroshiro128++ streams of a run to the
-//                               segment start (msim_jump.h) and write one 32-bit word per block:
-//                                 interval_ms << 7 | code,  code = floor(u / PERC_MULTIPLIER) in [0, 100]
-//                               (simulation.h:205-221). The word does not depend on the network, so a sweep
-//                               draws once per run and every point decodes code -> finder with its own
-//                               table; weighted networks store the finder itself (code < 16).
-//                               Layout: tiles of 32 words per run, [block / 32][run][32], so a worker's
-//                               stores and an engine lane's loads both stay inside 128-byte lines.
-//   E1 msim_sel_kernel          one lane per (point, run): the settled form + entity engine over the run's
-//                               draws, made in-lane (a single network: no word stream) or read from D1's
-//                               words (a multi-point sweep); per-run MinerStats terms reduced per workgroup
-//                               (fixed-point integers).
+//   E1 msim_sel_kernel          one lane per (point, run): the settled form (msim_selm.h) with the draws made
+//                               in-lane; finds the settled form cannot take are queued per workgroup and
+//                               stepped through the entity engine by whichever wave of the workgroup is
+//                               free (msim_sel_kernels.hip sel_pool), so engine work runs in full waves;
+//                               per-run MinerStats terms reduced per workgroup (fixed-point integers).
 //   E2 msim_sel_retry_kernel    one lane per flagged run: the engine with wide capacities and the draws
 //                               recomputed in-lane from the seeds, atomically added to per-point sums.
 //   G  msim_gen_kernel          the runs E2 could not finish (a chain outgrew the 16-height window: a
@@ -26,8 +19,6 @@
 #include "msim_sel.h"
 
 namespace msim {
-
-constexpr uint32_t SEL_TILE = 32;  // words per (run, tile)
 
 // Capacities of E1: one selfish miner (the mixed schedule): 1 hot active slot, 4 reveal groups, 1 in-flight
 // block per hot slot; several selfish miners (the engine alone): 2 / 4 / 2. Both are backed by SEL_NC cold
@@ -51,21 +42,11 @@ struct SelParams {
     // carry the finder and ccum[k] = k + 1. Unused entries 0xFFFFFFFF; a result >= m falls through.
     uint32_t ccum[MAXM];
     uint32_t macro;      // 1: one selfish miner, every propagation >= 1 ms (the settled form applies, msim_selm.h)
-    uint32_t xth;        // waiting lanes that start an engine phase (mixed schedule, msim_sel_kernels.hip)
+    uint32_t xth;        // waiting lanes that start an engine phase (per-wave mixed schedule, E2)
+    // the workgroup pool of E1 (msim_sel_kernels.hip sel_pool): queued runs that start an engine phase, the
+    // active engine lanes below which a phase stops taking more runs, and the phase's refill iterations
+    uint32_t pool_q, pool_lmin, pool_iters;
     uint32_t pad3;
-};
-
-struct WordArgs {
-    const LogTab *logt;
-    const uint32_t *jump;  // nseg * 128 columns of 4 words
-    uint64_t run_begin;    // absolute index of the slice's first run
-    uint32_t seed_base;
-    uint32_t nr, seg, nseg;
-    uint32_t mode;         // 0: code = floor(u / PERC_MULTIPLIER); 1: code = finder (weighted network)
-    uint32_t W, m;
-    uint64_t mult;
-    uint64_t cum[MAXM];
-    uint32_t *words;       // [nb / 32][nr][32]
 };
 
 struct SelArgs {
@@ -77,8 +58,6 @@ struct SelArgs {
     uint64_t run_begin;
     uint32_t seed_base;
     uint32_t s0, sn;        // slice: runs [s0, s0 + sn) of every point (s0 a multiple of TPB)
-    uint32_t nr, nb;        // word geometry of the slice
-    const uint32_t *words;  // null: E1 draws in-lane (SelFastDraw) and D1 does not run
     const LogTab *logt;     // interval table of the in-lane draws
     uint64_t *partials;     // [n_points][wpp][6M]
     uint64_t *retry_sums;   // [n_points][6M]
@@ -95,49 +74,6 @@ struct SelArgs {
     uint32_t uni;           // every point of this E1 launch has one propagation delay for all miners
 };
 
-struct SelLayout {
-    uint32_t nr;    // runs per slice (multiple of 256)
-    uint32_t seg;   // blocks per draw worker (multiple of SEL_TILE)
-    uint32_t nseg;  // draw workers per run
-    uint32_t nb;    // pre-generated blocks per run
-    size_t words_bytes;
-};
-
-// Slice geometry: nb >= mu + 8 sigma + 64 blocks (a run needing more is flagged and recomputed in E2);
-// draw workers per run chosen to fill `slots` resident waves in whole rounds (as msim_pipeline.h).
-inline SelLayout sel_layout_for(int64_t duration_ms, uint64_t n_runs, double budget, uint32_t slots)
-{
-    SelLayout L;
-    const double D = (double)duration_ms;
-    const double mu = D / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
-    const double need = mu + 8.0 * sd + 64.0;
-    const uint64_t want = (n_runs + 255) / 256 * 256;
-    uint64_t cap = (uint64_t)(budget / ((need + 2.0 * 512.0) * 4.0)) / 256 * 256;
-    if (cap < 256) cap = 256;
-    L.nr = (uint32_t)(want < cap ? want : cap);
-    if (slots < 1) slots = 1;
-    const double rows = L.nr / 64.0;
-    uint32_t best_w = 1;
-    double best_f = 1e300;
-    for (uint32_t w = 1; w <= 256; ++w) {
-        const uint32_t sg = (uint32_t)ceil(need / w / SEL_TILE) * SEL_TILE;
-        if (sg < 512 && w > 1) break;
-        const double f = ceil(rows * w / slots) * (sg + 25.0);
-        if (f < best_f * 0.999) {
-            best_f = f;
-            best_w = w;
-        }
-    }
-    L.nseg = best_w;
-    L.seg = (uint32_t)ceil(need / best_w / SEL_TILE) * SEL_TILE;
-    if (L.seg < 2 * SEL_TILE) L.seg = 2 * SEL_TILE;
-    L.nb = L.nseg * L.seg;
-    L.words_bytes = (size_t)L.nb * L.nr * 4;
-    return L;
-}
-
-hipError_t launch_word_draws(const WordArgs &a, hipStream_t s);
-hipError_t word_draws_blocks_per_cu(int *blocks);
 // E1 / E2 for miner count m and selfish class (1, 2, 4); dispatch in msim_common.hip.
 hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
