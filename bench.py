@@ -34,17 +34,26 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL = 52594.92
 
 
-# HBM bytes per launch of the dominant kernel at the default run counts, from rocprofv3 PMC passes
-# (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, separate passes; c2: profiles/r03/final/pmc_final.md,
-# K1 of round 3; c5: profiles/r01/pmc_f1.md). PMC counters cannot be collected inside this process; these
-# are the recorded values of the same command.
-TRAFFIC_PMC = {("c2", 32768): 4.98e8, ("c5", 65536): 9.128e8}
-TRAFFIC_SRC = {"c2": "profiles/r03/final/pmc_final.md", "c5": "profiles/r01/pmc_f1.md"}
-# SQ_INSTS_VALU (wave instructions) per launch of the kernels the live timing covers, same passes
-# (c2: K1 only, timed by k1_ms; c3: E1 = the whole launch, timed by kernel_ms): the counter-based
-# VALU issue fraction = instructions x 64 lanes / time / peak, reported beside the SURVEY 8(d) convention.
-VALU_INSTS_PMC = {("c2", 32768): (1.778e9, "k1"), ("c3", 131072): (2.526e10, "launch"),
-                  ("c5", 65536): (5.81e9, "k1")}
+# PMC constants of the dominant kernel per launch at the default run counts, from rocprofv3 --pmc passes of
+# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc_r04.sh: FETCH_SIZE, WRITE_SIZE and the
+# SQ set in separate passes; files under profiles/r04/pmc/, values there summed over 2 launches, KB). PMC counters
+# cannot be collected inside the timed process: these are the recorded values of the same kernel.
+#   traffic = FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of wide reads, MI355X_MICROARCH.md §HBM)
+#             + WRITE_SIZE, bytes per launch;
+#   valu    = SQ_INSTS_VALU (wave instructions) per launch: the counter-based VALU issue fraction is
+#             valu x 64 lanes / the kernel's live time / peak, reported beside the SURVEY 8(d) convention.
+PMC = {
+    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "fetch_kb": 21265.6 / 2, "write_kb": 883911 / 2,
+                    "valu": 3.55634e9 / 2, "src": "profiles/r04/pmc/pmc_c2.txt"},
+    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "fetch_kb": 9.40858e6 / 2,
+                     "write_kb": 4.6686e7 / 2, "valu": 4.99608e10 / 2, "src": "profiles/r04/pmc/pmc_c3.txt"},
+    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "fetch_kb": 3309 / 2, "write_kb": 1.82864e6 / 2,
+                    "valu": 1.07196e10 / 2, "src": "profiles/r04/pmc/pmc_c5.txt"},
+}
+# rocprofv3 --kernel-trace --stats summaries of the exact bench commands (default streams and --streams 1), whose
+# average duration of the dominant kernel is the file-backed counterpart of the live HIP-event time in the line.
+ROCPROF = {"c2": "profiles/r04/final/rocprof_c2_s{s}.md", "c3": "profiles/r04/final/rocprof_c3_s{s}.md",
+           "c5": "profiles/r04/final/rocprof_c5_s{s}.md"}
 
 
 def w_blk(m: int) -> int:
@@ -331,34 +340,32 @@ def main() -> None:
     assert tm["launches"] == args.steps, tm
     kern_ms = tm["launch_ms"] / args.steps  # all kernels of one msim_launch (K1+K2+K3+finalize)
     k1_ms = tm["draws_ms"] / args.steps
+    e1_ms = tm.get("engine_ms", 0.0) / args.steps  # E1 kernels (selfish networks)
     total = sum(ln["total"] for ln in lanes)
     fails = sum(ln["fails"] for ln in lanes)
-    t = torch.tensor([elapsed, kern_ms, k1_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kern_ms, k1_ms, e1_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(fails)
-    elapsed, kern_ms, k1_ms = float(t[0]), float(t[1]), float(t[2])
+    elapsed, kern_ms, k1_ms, e1_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
     if int(fails.item()) != 0:
         raise SystemExit(f"{int(fails.item())} runs exceeded the compact state capacity")
 
     pipe = sim.pipeline_info(n)
-    issue_frac, issue_src = None, None
-    if (args.config, n) in VALU_INSTS_PMC:
-        insts, which = VALU_INSTS_PMC[(args.config, n)]
-        t_s = (k1_ms if which == "k1" else kern_ms) / 1e3
-        issue_frac = round(insts * 64 / t_s / VALU_PEAK_LANE_OPS, 4) if t_s > 0 else None
-        issue_src = (f"SQ_INSTS_VALU {insts:.4g} per launch (profiles/r03/final/pmc_final.md) x 64 lanes / live "
-                     f"{'K1' if which == 'k1' else 'launch'} time / peak")
-    runs_total = args.steps * n * world
-    value = runs_total / elapsed
-    # Roofline of the dominant kernel: the draw kernel (K1 / W1) for honest networks, which does every fast
-    # block's whole work; for selfish networks the whole launch (D1 draws + E1 engine). Live HIP-event time
-    # on the launch stream; with --streams 2 a launch shares the GPU with the other stream's, so this
-    # duration (and rocprof's, which agrees) is longer than the kernel alone.
+    # Roofline of the dominant kernel: the draw kernel for honest networks (K1 / W1: it does every fast block's
+    # whole work), E1 for selfish ones. Its time is the live HIP-event time on the launch stream (with two
+    # streams a launch shares the GPU with the other stream's, so this duration is longer than the kernel
+    # alone; ROCPROF's summary of the same command agrees with it).
     honest = pipe.get("uses_pipeline") in (1, 2)
-    dom_ms = k1_ms if honest and k1_ms > 0 else kern_ms
+    dom_ms = k1_ms if honest and k1_ms > 0 else (e1_ms if e1_ms > 0 else kern_ms)
+    pmc = PMC.get((args.config, n))
+    issue_frac = None
+    if pmc and dom_ms > 0:
+        issue_frac = round(pmc["valu"] * 64 / (dom_ms / 1e3) / VALU_PEAK_LANE_OPS, 4)
     per_gpu_kernel_rate = n / (dom_ms / 1e3)  # run-years/s of the dominant kernel on one GPU
     achieved = per_gpu_kernel_rate * BLOCKS_PER_RUN_YEAR * w_blk(m)  # algorithmic lane-ops/s per GPU
+    runs_total = args.steps * n * world
+    value = runs_total / elapsed
     # sanity: aggregate share of miner 0 (integer sums, exact across ranks)
     tot = total.cpu().tolist()
     share0 = (tot[0][2] + tot[0][3] * 2.0**-32) / (runs_total) * 100
@@ -394,16 +401,17 @@ def main() -> None:
                 "peak": round(VALU_PEAK_LANE_OPS / 1e12, 2),
                 "unit": "T lane-op/s",
                 "frac": round(achieved / VALU_PEAK_LANE_OPS, 5),
-                "traffic": TRAFFIC_PMC.get((args.config, n)),
-                "traffic_source": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this command, recorded in "
-                                   f"{TRAFFIC_SRC.get(args.config)} (bytes per launch of the draw kernel)")
-                if (args.config, n) in TRAFFIC_PMC else None,
+                "traffic": round(pmc["fetch_kb"] * 1024 * 2 + pmc["write_kb"] * 1024) if pmc else None,
+                "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of {pmc['kernel']} per launch "
+                                   f"(serial bench, {pmc['src']})") if pmc else None,
                 "valu_issue_frac_pmc": issue_frac,
-                "valu_issue_source": issue_src,
+                "valu_issue_source": (f"SQ_INSTS_VALU {pmc['valu']:.4g} per launch ({pmc['src']}) x 64 lanes / "
+                                      f"dominant_ms / peak") if pmc else None,
                 "kernel": ("W1 msim_wide_draws_kernel" if sim.wide else "K1 msim_draws_kernel" if honest else
-                           "msim_launch = D1 msim_word_draws_kernel + E1 msim_sel_kernel + E2 retries + finalize") +
-                          " (HIP events on the launch stream)",
+                           "E1 msim_sel_kernel (settled form + entity engine)") + " (HIP events on the launch stream)",
                 "dominant_ms": round(dom_ms, 4),
+                "dominant_ms_file": ROCPROF[args.config].format(s=0 if ns == 2 else 1)
+                if args.config in ROCPROF and ns in (1, 2) and args.steps == 40 else None,
                 "kernel_ms": round(kern_ms, 4),
                 "k1_ms": round(k1_ms, 4),
                 "k1_share": round(k1_ms / kern_ms, 4) if kern_ms > 0 else None,

@@ -409,18 +409,6 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
     for (uint32_t k = 0; k < n; ++k) pmax = miners[k].propagation_ms > pmax ? miners[k].propagation_ms : pmax;
     sp->xth = pmax <= 2000 ? 16u : (pmax <= 10000 ? 32u : 48u);
     if (const char *e = getenv("MSIM_SEL_XTH")) sp->xth = (uint32_t)atoi(e);  // A/B override
-    // E1's workgroup pool (msim_sel_kernels.hip sel_pool); A/B overrides MSIM_SEL_POOL="q,lmin,iters"
-    sp->pool_q = 32;
-    sp->pool_lmin = 16;
-    sp->pool_iters = 24;
-    if (const char *e = getenv("MSIM_SEL_POOL")) {
-        unsigned q = 0, l = 0, it = 0;
-        if (sscanf(e, "%u,%u,%u", &q, &l, &it) == 3) {
-            sp->pool_q = q;
-            sp->pool_lmin = l;
-            sp->pool_iters = it;
-        }
-    }
 }
 
 struct SelGroupDev {

@@ -355,6 +355,23 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
     return src[(size_t)(CNT_WORDS - 1) * stride] >> 16;
 }
 
+// K3 phase timing (diagnostic builds only, -DK3_PROF=1: scripts/build_variant.sh): clock at each phase of
+// combine_run for the first lane of a few workgroups.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(K3_PROF) && K3_PROF
+#define K3T(i) k3t[i] = clock64()
+#define K3T_DECL uint64_t k3t[8] = {0, 0, 0, 0, 0, 0, 0, 0}; K3T(0)
+#define K3T_PRINT                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x % 16 == 0)                                                               \
+        printf("K3PROF blk %u seg %llu segcnt %llu groups %llu redraw %llu prevgrp %llu eps %llu\n", blockIdx.x, \
+               (unsigned long long)(k3t[1] - k3t[0]), (unsigned long long)(k3t[2] - k3t[1]),                    \
+               (unsigned long long)(k3t[3] - k3t[2]), (unsigned long long)(k3t[4] - k3t[3]),                    \
+               (unsigned long long)(k3t[5] - k3t[4]), (unsigned long long)(k3t[6] - k3t[5]))
+#else
+#define K3T(i)
+#define K3T_DECL
+#define K3T_PRINT
+#endif
+
 // Combine one run r of a slice. Returns false when the run must be recomputed by the retry path.
 // nsw: K3_SEG_MAX words of per-run scratch at stride nss (device: the lane's LDS column).
 constexpr uint32_t K3_SEG_MAX = 32;
@@ -363,6 +380,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
                          uint32_t *nsw, size_t nss)
 {
     const int64_t D = p.duration_ms;
+    K3T_DECL;
 #pragma unroll
     for (int k = 0; k < M; ++k) {
         F[k] = 0;
@@ -385,9 +403,33 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             }
         }
     }
+    K3T(1);
     if (e < (int)a.band_lo) return false;  // past the pre-generated draws or outside the band
-    for (int j = 0; j < e; ++j)
-        if (add_packed<M>(F, a.segcnt + (size_t)j * CNT_WORDS * a.nr + r, a.nr)) return false;  // fell through
+    {  // per-owner counts of the segments before e, KB segments' loads in flight together (no early exit
+       // between them: a fall-through in any of them is checked once at the end)
+        uint32_t ft = 0;
+        for (int j0 = 0; j0 < e; j0 += (int)KB) {
+            uint32_t c[KB][CNT_WORDS];
+#pragma unroll
+            for (uint32_t j = 0; j < KB; ++j)
+#pragma unroll
+                for (uint32_t w = 0; w < CNT_WORDS; ++w)
+                    c[j][w] = (j0 + (int)j < e && (w < (uint32_t)(M + 1) / 2 || w == CNT_WORDS - 1))
+                                  ? a.segcnt[((size_t)(j0 + (int)j) * CNT_WORDS + w) * a.nr + r]
+                                  : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < KB; ++j) {
+#pragma unroll
+                for (int w = 0; w < (M + 1) / 2; ++w) {
+                    F[2 * w] += c[j][w] & 0xFFFFu;
+                    if (2 * w + 1 < M) F[2 * w + 1] += c[j][w] >> 16;
+                }
+                ft |= c[j][CNT_WORDS - 1] >> 16;
+            }
+        }
+        if (ft) return false;  // PickFinder fell through (owner 15): the retry kernel reports it
+    }
+    K3T(2);
     // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Group sums
     // KG at a time, as above (a segment has up to a few hundred groups).
     constexpr uint32_t KG = 32;
@@ -406,6 +448,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         }
     }
     if (G == a.gps) return false;
+    K3T(3);
     if (add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr)) return false;
     const uint32_t bg = (uint32_t)e * a.seg + G * GROUP;
     uint32_t n_end = 0, klast = 15u;
@@ -432,6 +475,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         }
     }
     if (!done) return false;
+    K3T(4);
     if (n_end == bg && n_end > 0) {  // the block before the end is the previous group's last one
         size_t pg;
         if (G > 0) pg = gb + G - 1;
@@ -448,6 +492,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     // a run waits for three rounds of memory latency instead of one per segment and two per episode; a run
     // with more than EP_MAX episodes up to its end segment (never at BASELINE sizes: ~rho * blocks, 9 for
     // configs[1]) takes the same walk one read at a time.
+    K3T(5);
     uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
     constexpr uint32_t EP_MAX = 32, SEG_MAX = K3_SEG_MAX;
     uint32_t tot = 0;
@@ -547,6 +592,8 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             }
         }
     }
+    K3T(6);
+    K3T_PRINT;
     // 4. The run ended quiet and its last block was a fast one: it counts only if it arrived by D.
     if (cursor != 0xFFFFFFFFu && n_end > 0 && cursor < n_end) {
         const uint32_t k = klast;

@@ -2,8 +2,6 @@
 // per miner count (MSIM_M).
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "msim_general_launch.h"
 #include "msim_kernels.h"
 #include "msim_reduce.h"
@@ -344,374 +342,23 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
     o.err = err;
 }
 
-// ------------------------------------------------------------------ E1's workgroup pool
-// Why. With one lane per run, every lane of a wave advances its own run in the settled form (msim_selm.h)
-// until one of its finds needs the entity engine. Engine episodes are rare (~82 per run-year at configs[2]),
-// short (5.6 events on average) and ~9x as costly per step as a settled-form step. Run per wave (the mixed
-// schedule above), an engine phase stepped ~16 waiting lanes until the longest episode ended: 7.4 of 64
-// lanes active on average, 32 % of E1's cycles (round 3, profiles/r03/e1ab/selprof_c3.txt).
-//
-// The pool moves a run between lanes instead. A run that needs the engine leaves its home lane: its
-// settled state (SelMacro, LDS s_mc) and its draw state (both xoroshiro128++ states and the held draws,
-// LDS x) are written to its SLOT (the home lane's index in the workgroup) and the slot is queued in an LDS
-// ring shared by the workgroup's four waves; its per-run counters already live in the slot's LDS columns
-// (s_cnt) and its cold engine slots in global memory indexed by the slot. Any wave of the workgroup whose
-// own lanes have run short of settled-form work, or that sees enough runs queued, becomes an engine worker:
-// its lanes claim queued slots, step the entity engine on them, and claim the next queued slot as soon as
-// their episode ends (the slot goes back to its home lane with the new settled state, or is finished), so
-// engine steps run on (nearly) full waves. Which lane computes which part of a run never changes a result:
-// every run performs its own sequence of transitions (tests/native/sel_host.cpp runs one lane alone).
-//
-// Synchronisation is LDS only (no global memory crosses lanes): a producer writes the slot's state, fences
-// (release, workgroup scope) and publishes the slot in the ring (slot + 1; 0 = empty) at a position
-// reserved with one atomic on `tail`; a consumer reserves ring positions with a compare-and-swap on `head`,
-// waits for the entry to be non-zero, clears it and fences (acquire) before reading the slot. Status words
-// tell a home lane that its run is back (PS_BACK) or finished (PS_DONE). Every wait is bounded: a wave that
-// waited 2^20 sleeps flags its away runs (SERR_SCHED: E2 recomputes them exactly), so the workgroup always
-// drains.
-enum : uint32_t { PS_QUEUED = 1u, PS_BACK = 2u, PS_DONE = 3u };
-constexpr uint32_t SERR_SCHED = 128u;  // a run whose pool hand-over did not complete (never observed)
-constexpr uint32_t POOL_QCAP = 2u * TPB;
-constexpr uint32_t POOL_NOSLOT = 0xFFFFFFFFu;
-constexpr uint32_t POOL_XW = 12;  // transfer words: RNG states (8), held intervals (3), held finders + count (1)
-constexpr uint32_t POOL_SPIN_MAX = 1u << 20;
-
-struct SelPool {
-    uint32_t st[TPB];           // slot status (PS_*), written when the slot leaves / returns to its home lane
-    uint32_t q[POOL_QCAP];      // ring of queued slots (slot + 1), 0 = empty
-    uint32_t head, tail;
-    uint32_t x[POOL_XW][TPB];   // the slot's draw state while it is away
-};
-
-#ifndef SEL_POOL
-#define SEL_POOL 1  // 0: the per-wave mixed schedule for every network (A/B)
-#endif
-#ifndef SEL_PSTEPS
-#define SEL_PSTEPS 2  // settled-form steps between pool checks
-#endif
-
-template <int M>
-struct SelPoolLds {
-    static constexpr int NW = SelMacro<M>::NW;
-    // the pool needs two workgroups per CU (two waves per SIMD): s_cnt, s_mc and the pool within 80 KiB
-    static constexpr size_t BYTES = (size_t)(4 * M + NW) * TPB * 4 + sizeof(SelPool) + 4096;
-    static constexpr bool FITS = SEL_POOL && BYTES <= 80 * 1024;
-};
-
-__device__ __forceinline__ uint32_t lds_load(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-__device__ __forceinline__ void lds_store(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELAXED); }
-__device__ __forceinline__ void fence_rel() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
-__device__ __forceinline__ void fence_acq() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
-__device__ __forceinline__ uint32_t lane_id()
-{
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-__device__ __forceinline__ uint32_t rank_in(uint64_t mask)
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-// Queued slots (head first: head never passes a tail read after it).
-__device__ __forceinline__ uint32_t pool_queued(const SelPool &pl)
-{
-    const uint32_t h = lds_load(&pl.head);
-    const uint32_t t = lds_load(&pl.tail);
-    return (uint32_t)__builtin_amdgcn_readfirstlane(t - h);
-}
-
-template <int M>
-__device__ __forceinline__ void xfer_save(const SelFifo<SelFastDraw<M>> &f, SelPool &pl, uint32_t slot)
-{
-    pl.x[0][slot] = (uint32_t)f.d.ri.s0;
-    pl.x[1][slot] = (uint32_t)(f.d.ri.s0 >> 32);
-    pl.x[2][slot] = (uint32_t)f.d.ri.s1;
-    pl.x[3][slot] = (uint32_t)(f.d.ri.s1 >> 32);
-    pl.x[4][slot] = (uint32_t)f.d.rp.s0;
-    pl.x[5][slot] = (uint32_t)(f.d.rp.s0 >> 32);
-    pl.x[6][slot] = (uint32_t)f.d.rp.s1;
-    pl.x[7][slot] = (uint32_t)(f.d.rp.s1 >> 32);
-    pl.x[8][slot] = f.I0;
-    pl.x[9][slot] = f.I1;
-    pl.x[10][slot] = f.I2;
-    pl.x[11][slot] = (f.k0 & 0xFFu) | ((f.k1 & 0xFFu) << 8) | ((f.k2 & 0xFFu) << 16) | (f.n << 24);
-}
-template <int M>
-__device__ __forceinline__ void xfer_load(SelFifo<SelFastDraw<M>> &f, const SelPool &pl, uint32_t slot)
-{
-    f.d.ri.s0 = (uint64_t)pl.x[0][slot] | ((uint64_t)pl.x[1][slot] << 32);
-    f.d.ri.s1 = (uint64_t)pl.x[2][slot] | ((uint64_t)pl.x[3][slot] << 32);
-    f.d.rp.s0 = (uint64_t)pl.x[4][slot] | ((uint64_t)pl.x[5][slot] << 32);
-    f.d.rp.s1 = (uint64_t)pl.x[6][slot] | ((uint64_t)pl.x[7][slot] << 32);
-    f.I0 = pl.x[8][slot];
-    f.I1 = pl.x[9][slot];
-    f.I2 = pl.x[10][slot];
-    const uint32_t w = pl.x[11][slot];
-    f.k0 = w & 0xFFu;
-    f.k1 = (w >> 8) & 0xFFu;
-    f.k2 = (w >> 16) & 0xFFu;
-    f.n = w >> 24;
-}
-
-// A slot's final counters (MinerStats inputs) in its LDS columns, best height and error in s_mc words 0-1.
-template <int M, class Env>
-__device__ __forceinline__ void pool_park(Env &env, const SelOut &r, uint32_t (*s_mc)[TPB], uint32_t slot)
-{
-#pragma unroll
-    for (int k = 0; k < M; ++k) {
-        env.set(C_F, (uint32_t)k, r.found[k]);
-        env.set(C_S, (uint32_t)k, r.stale[k]);
-    }
-    s_mc[0][slot] = r.best_height;
-    s_mc[1][slot] = r.err;
-}
-
-// The pool schedule of one workgroup (one point). Every lane runs it (a lane without a run starts done and
-// still serves as an engine worker). On return the lane's own run is finished: counters in its s_cnt
-// columns, best height / error in s_mc[0..1][tid].
-template <int M, class SelT, bool UNI>
-__device__ __forceinline__ void sel_pool(const SelArgs &a, const SelParams *P, SelFifo<SelFastDraw<M>> &src, uint32_t (*s_cnt)[TPB],
-                         const int64_t *s_prop, uint32_t (*s_mc)[TPB], SelPool &pl, size_t lane0, bool active)
-{
-    const uint32_t tid = threadIdx.x;
-    const int64_t D = P->duration_ms;
-    const uint32_t sid = P->sids[0];
-    const int64_t ps = P->prop[sid];
-    const uint32_t qe = (uint32_t)__builtin_amdgcn_readfirstlane(P->pool_q >= 1u && P->pool_q <= 64u ? P->pool_q : 32u);
-    const uint32_t lmin = (uint32_t)__builtin_amdgcn_readfirstlane(P->pool_lmin <= 64u ? P->pool_lmin : 16u);
-    const int iters = (int)__builtin_amdgcn_readfirstlane(P->pool_iters >= 1u ? P->pool_iters : 24u);
-    SelDevEnv<M, UNI> env{&s_cnt[0][tid], s_prop, P->prop[0], P->uniform_prop != 0, a.cold + lane0 + tid, a.cold_lanes};
-    int mode = 3;  // 0 settled form here, 1 away (queued or in an engine), 3 done
-    SelMacro<M> mc;
-    if (!active) {
-        s_mc[0][tid] = 0;
-        s_mc[1][tid] = 0;
-    } else if (a.force_retry) {
-        s_mc[0][tid] = 0;
-        s_mc[1][tid] = SERR_CAP;
-    } else if (!mc.begin(src)) {
-        s_mc[0][tid] = 0;
-        s_mc[1][tid] = SERR_DRAWS;
-    } else if (mc.T >= D) {
-        SelOut r;
-        mc.finish(env, sid, r);
-        pool_park<M>(env, r, s_mc, tid);
-    } else {
-        mode = 0;
-    }
-#if SEL_PROF
-    uint64_t pr_set = 0, pr_setl = 0, pr_eng = 0, pr_engl = 0, pr_ph = 0, pr_spin = 0;
-    const uint64_t pr_t0 = clock64();
-    uint64_t pr_te = 0;
-#endif
-    uint32_t spins = 0;
-    for (;;) {
-        // 1. settled-form steps (an inner loop, so that only the settled form's state is live in it) until
-        // this wave has no settled-form work left or enough runs wait for an engine; a run that needs the
-        // engine is handed to the pool, a run that comes back is taken up again
-        if (__builtin_amdgcn_ballot_w64(mode == 0) != 0ull) {
-            for (;;) {
-                bool hand = false;
-#pragma unroll
-                for (int u = 0; u < SEL_PSTEPS; ++u) {
-#if SEL_PROF
-                    ++pr_set;
-                    pr_setl += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 0));
-#endif
-                    if (mode == 0) {
-                        const int r = mc.step(env, src, D, sid, ps);
-                        if (r == 2) {
-                            SelOut q;
-                            mc.finish(env, sid, q);
-                            pool_park<M>(env, q, s_mc, tid);
-                            mode = 3;
-                        } else if (r == 1) {
-                            mc.save(&s_mc[0][tid], TPB);
-                            xfer_save<M>(src, pl, tid);
-                            lds_store(&pl.st[tid], PS_QUEUED);
-                            hand = true;
-                            mode = 1;
-                        }
-                    }
-                }
-                const uint64_t hm = __builtin_amdgcn_ballot_w64(hand);
-                if (hm != 0ull) {
-                    const uint32_t first = (uint32_t)__builtin_ctzll(hm);
-                    uint32_t base = 0;
-                    if (lane_id() == first)
-                        base = __atomic_fetch_add(&pl.tail, (uint32_t)__builtin_popcountll(hm), __ATOMIC_RELAXED);
-                    base = __builtin_amdgcn_readlane(base, first);
-                    if (hand) {
-                        fence_rel();  // the slot's state before its ring entry
-                        lds_store(&pl.q[(base + rank_in(hm)) & (POOL_QCAP - 1u)], tid + 1u);
-                    }
-                }
-                if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull || pool_queued(pl) >= qe) break;
-            }
-        }
-        // 2. runs that came back from an engine (or finished there)
-        if (__builtin_amdgcn_ballot_w64(mode == 1) != 0ull) {
-            if (mode == 1) {
-                const uint32_t v = lds_load(&pl.st[tid]);
-                if (v == PS_BACK) {
-                    fence_acq();
-                    mc.load(&s_mc[0][tid], TPB);
-                    xfer_load<M>(src, pl, tid);
-                    mode = 0;
-                } else if (v == PS_DONE) {
-                    mode = 3;
-                }
-            }
-        }
-        // 3. become an engine worker when enough runs wait, or when this wave has no settled-form work left
-        const uint32_t nset = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 0));
-        const uint32_t qn = pool_queued(pl);
-        if (qn >= qe || (nset == 0u && qn > 0u)) {
-            spins = 0;
-#if SEL_PROF
-            ++pr_ph;
-            const uint64_t pc0 = clock64();
-#endif
-            // this wave's settled runs wait in their slots: no settled-form register is live in the phase
-            if (mode == 0) {
-                mc.save(&s_mc[0][tid], TPB);
-                xfer_save<M>(src, pl, tid);
-            }
-            {
-                uint32_t es = POOL_NOSLOT;
-                SelT s;
-                SelFifo<SelFastDraw<M>> ex = src;  // the drawer's tables; per-run state comes with each slot
-                SelDevEnv<M, UNI> ee = env;
-                bool refill = true;
-                for (int it = 0;; ++it) {
-                    if (refill) {
-                        const uint64_t fm = __builtin_amdgcn_ballot_w64(es == POOL_NOSLOT);
-                        if (fm != 0ull) {
-                            const uint32_t first = (uint32_t)__builtin_ctzll(fm);
-                            uint32_t h = 0, c = 0;
-                            if (lane_id() == first) {
-                                const uint32_t nfree = (uint32_t)__builtin_popcountll(fm);
-                                for (int tries = 0; tries < 64; ++tries) {
-                                    h = lds_load(&pl.head);
-                                    const uint32_t t = lds_load(&pl.tail);
-                                    c = t - h < nfree ? t - h : nfree;
-                                    if (c == 0u) break;
-                                    uint32_t exp = h;
-                                    if (__atomic_compare_exchange_n(&pl.head, &exp, h + c, false, __ATOMIC_RELAXED,
-                                                                    __ATOMIC_RELAXED))
-                                        break;
-                                    c = 0;
-                                }
-                            }
-                            h = __builtin_amdgcn_readlane(h, first);
-                            c = __builtin_amdgcn_readlane(c, first);
-                            const uint32_t rk = rank_in(fm);
-                            if (es == POOL_NOSLOT && rk < c) {
-                                uint32_t *e = &pl.q[(h + rk) & (POOL_QCAP - 1u)];
-                                uint32_t v = lds_load(e);
-                                for (uint32_t w = 0; v == 0u && w < POOL_SPIN_MAX; ++w) {
-                                    __builtin_amdgcn_s_sleep(1);
-                                    v = lds_load(e);
-                                }
-                                lds_store(e, 0u);
-                                fence_acq();
-                                if (v != 0u) {
-                                    es = v - 1u;
-                                    SelMacro<M> t;
-                                    t.load(&s_mc[0][es], TPB);
-                                    xfer_load<M>(ex, pl, es);
-                                    ee.c = &s_cnt[0][es];
-                                    ee.cb = a.cold + lane0 + es;
-                                    t.to_exact(ee, s, P->m, P->sids);
-                                }
-                            }
-                        }
-                    }
-                    const uint64_t am = __builtin_amdgcn_ballot_w64(es != POOL_NOSLOT);
-                    if (am == 0ull) break;
-#if SEL_PROF
-                    ++pr_eng;
-                    pr_engl += __builtin_popcountll(am);
-#endif
-                    if (es != POOL_NOSLOT) {
-                        const bool live = s.step(ee, ex, D);
-                        if (!live) {
-                            SelOut r;
-                            s.finish(ee, D, r);
-                            pool_park<M>(ee, r, s_mc, es);
-                            fence_rel();
-                            lds_store(&pl.st[es], PS_DONE);
-                            es = POOL_NOSLOT;
-                        } else {
-                            SelMacro<M> tb;
-                            if (tb.take_back(ee, s, sid)) {
-                                if (tb.T >= D) {
-                                    SelOut r;
-                                    tb.finish(ee, sid, r);
-                                    pool_park<M>(ee, r, s_mc, es);
-                                    fence_rel();
-                                    lds_store(&pl.st[es], PS_DONE);
-                                } else {
-                                    ex.fill();  // the settled form starts every step with two held draws
-                                    tb.save(&s_mc[0][es], TPB);
-                                    xfer_save<M>(ex, pl, es);
-                                    fence_rel();
-                                    lds_store(&pl.st[es], PS_BACK);
-                                }
-                                es = POOL_NOSLOT;
-                            }
-                        }
-                    }
-                    // keep claiming while the phase is young and full enough; then drain what is in hand
-                    const uint32_t act = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(es != POOL_NOSLOT));
-                    const uint32_t q2 = pool_queued(pl);
-                    refill = refill && it + 1 < iters && act + q2 >= lmin;
-                }
-            }
-            if (mode == 0) {
-                mc.load(&s_mc[0][tid], TPB);
-                xfer_load<M>(src, pl, tid);
-            }
-#if SEL_PROF
-            pr_te += clock64() - pc0;
-#endif
-            continue;
-        }
-        if (nset == 0u) {
-            if (__builtin_amdgcn_ballot_w64(mode != 3) == 0ull) break;  // every run of this wave is finished
-            // every unfinished run of this wave is in another wave's engine: wait for it
-#if SEL_PROF
-            ++pr_spin;
-#endif
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > POOL_SPIN_MAX) {
-                if (mode == 1) {
-                    s_mc[1][tid] = SERR_SCHED;
-                    mode = 3;
-                }
-            }
-        } else {
-            spins = 0;
-        }
-    }
-#if SEL_PROF
-    if (blockIdx.x < 2 && (tid & 63u) == 0u)
-        printf("POOLPROF blk %u wave %u total %llu | settled iters %llu lanes %llu | engine phases %llu cyc %llu iters %llu lanes %llu | spins %llu\n",
-               blockIdx.x, tid / 64u, (unsigned long long)(clock64() - pr_t0), (unsigned long long)pr_set,
-               (unsigned long long)pr_setl, (unsigned long long)pr_ph, (unsigned long long)pr_te,
-               (unsigned long long)pr_eng, (unsigned long long)pr_engl, (unsigned long long)pr_spin);
-#endif
-}
-
 // E1: one lane per (point, run of the slice); workgroups never straddle points. The lane makes its draws
-// itself (SelFastDraw). One selfish miner with the settled form: the workgroup pool (sel_pool) when its LDS
-// fits two workgroups per CU, else the per-wave mixed schedule; several selfish miners: the engine alone.
+// itself (SelFastDraw). One selfish miner: the mixed schedule (settled form + per-wave engine phases);
+// several selfish miners: the engine alone.
+//
+// Measured and rejected (round 4, profiles/r04/e1pool): a WORKGROUP pool that hands a run needing the engine
+// to whichever of the workgroup's four waves is free (the run's settled and draw state through LDS, an LDS
+// ring of queued runs), so that engine steps run on fuller waves. Exact, but slower on configs[2]: 80-125 ms
+// per 131 072-run launch against 57.5 ms, whatever the queue threshold / refill floor / phase length. An
+// engine step costs the same per ACTIVE lane (~1 300 cycles per lane-event at 7 or at 15 active lanes: the
+// step is a chain of dependent LDS / cold-slot accesses whose latency grows with the divergent paths taken),
+// so fuller engine waves saved nothing, while runs waited longer away from their lanes (32 instead of 57
+// lanes active per settled-form step).
 template <int M, int NS, int NA, int NG, int NQ, int NC, bool UNI>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_sel_kernel(const SelArgs a)
 {
-    constexpr bool POOL = NS == 1 && SelPoolLds<M>::FITS;
     __shared__ uint32_t s_cnt[4 * M][TPB];
-    __shared__ uint32_t s_mc[NS == 1 ? SelMacro<M>::NW : 1][TPB];
-    __shared__ std::conditional_t<POOL, SelPool, uint32_t> s_pool;
+    __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
     __shared__ int64_t s_prop[MAXM];
     __shared__ uint8_t s_lut[128];
     __shared__ LogTab s_log[1];
@@ -731,17 +378,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
     }
 #pragma unroll
     for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
-    if constexpr (POOL) {
-        s_pool.q[tid] = 0u;
-        s_pool.q[tid + TPB] = 0u;
-        s_pool.st[tid] = 0u;
-        if (tid == 0) s_pool.head = s_pool.tail = 0u;
-    }
     __syncthreads();
     const uint32_t lr = blk * TPB + tid;
     const bool active = lr < a.sn;
     const uint32_t rel = a.s0 + lr;
-    const size_t lane0 = (size_t)(blockIdx.x / wps) * wps * TPB + (size_t)blk * TPB;  // cold slots: lane0 + slot
+    const size_t lane0 = (size_t)(blockIdx.x / wps) * wps * TPB + (size_t)blk * TPB;  // cold slots: lane0 + tid
     const uint64_t run = a.run_begin + rel;
     SelFifo<SelFastDraw<M>> src;
     src.d.ri = rng_seed(seed_interval(a.seed_base, run));
@@ -753,28 +394,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
     src.d.wt = P->W != 100u;
     src.n = 0;
     SelOut o;
-    bool have = false;
-    if constexpr (POOL) {
-        if (P->macro != 0u) {  // wave-uniform (one point per workgroup)
-            sel_pool<M, Sel<M, NS, NA, NG, NQ, NC>, UNI>(a, P, src, s_cnt, s_prop, s_mc, s_pool, lane0, active);
-#pragma unroll
-            for (int k = 0; k < M; ++k) {
-                o.found[k] = s_cnt[C_F * M + k][tid];
-                o.stale[k] = s_cnt[C_S * M + k][tid];
-            }
-            o.best_height = s_mc[0][tid];
-            o.err = s_mc[1][tid];
-            have = true;
-        }
-    }
-    if (!have && active) {
+    if (active) {
         SelDevEnv<M, UNI> env{&s_cnt[0][tid], s_prop, P->prop[0], P->uniform_prop != 0, a.cold + lane0 + tid, a.cold_lanes};
         const int64_t D = P->duration_ms;
         if (a.force_retry) {
             o.err = SERR_CAP;
-        } else if constexpr (NS == 1 && !POOL) {
+        } else if constexpr (NS == 1) {
             sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid]);
-        } else {  // several selfish miners, or no settled form (a zero delay): the engine alone
+        } else {  // several selfish miners: the engine alone
             Sel<M, NS, NA, NG, NQ, NC> s;
             s.init(P->m, P->sids);
             s.begin(src);

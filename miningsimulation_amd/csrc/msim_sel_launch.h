@@ -2,10 +2,9 @@
 // selfish miners (BASELINE configs[2], configs[3]).
 //
 //   E1 msim_sel_kernel          one lane per (point, run): the settled form (msim_selm.h) with the draws made
-//                               in-lane; finds the settled form cannot take are queued per workgroup and
-//                               stepped through the entity engine by whichever wave of the workgroup is
-//                               free (msim_sel_kernels.hip sel_pool), so engine work runs in full waves;
-//                               per-run MinerStats terms reduced per workgroup (fixed-point integers).
+//                               in-lane, engine phases per wave for the finds it cannot take (the mixed
+//                               schedule, msim_sel_kernels.hip); per-run MinerStats terms reduced per
+//                               workgroup (fixed-point integers).
 //   E2 msim_sel_retry_kernel    one lane per flagged run: the engine with wide capacities and the draws
 //                               recomputed in-lane from the seeds, atomically added to per-point sums.
 //   G  msim_gen_kernel          the runs E2 could not finish (a chain outgrew the 16-height window: a
@@ -43,9 +42,6 @@ struct SelParams {
     uint32_t ccum[MAXM];
     uint32_t macro;      // 1: one selfish miner, every propagation >= 1 ms (the settled form applies, msim_selm.h)
     uint32_t xth;        // waiting lanes that start an engine phase (per-wave mixed schedule, E2)
-    // the workgroup pool of E1 (msim_sel_kernels.hip sel_pool): queued runs that start an engine phase, the
-    // active engine lanes below which a phase stops taking more runs, and the phase's refill iterations
-    uint32_t pool_q, pool_lmin, pool_iters;
     uint32_t pad3;
 };
 

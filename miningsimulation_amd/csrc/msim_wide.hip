@@ -59,24 +59,6 @@ __device__ __forceinline__ uint64_t wave_excl_scan(uint64_t x, uint32_t lane)
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); __builtin_amdgcn_wave_barrier(); }
 
-// The per-run LDS histogram holds two miners' 16-bit counts per word (a run has fewer than 2^16 blocks,
-// so neither half carries into the other): miner f's count is bits 16 (f & 1) .. of word f >> 1, and a
-// +1 / -1 is one ds_add_u32 of +-(1 << 16 (f & 1)). Half the LDS of one u32 per miner lets twice the runs
-// share a workgroup's tables.
-// Networks whose runs can draw 2^16 blocks or more (durations beyond ~14 months) keep one u32 per miner.
-template <bool PACK>
-__device__ __forceinline__ void hist_add(uint32_t *h, uint32_t f, uint32_t d)
-{
-    if constexpr (PACK) atomicAdd(&h[f >> 1], d << ((f & 1u) << 4));
-    else atomicAdd(&h[f], d);
-}
-template <bool PACK>
-__device__ __forceinline__ uint32_t hist_get(const uint32_t *h, uint32_t f)
-{
-    if constexpr (PACK) return (h[f >> 1] >> ((f & 1u) << 4)) & 0xFFFFu;
-    else return h[f];
-}
-
 struct W1Lds {
     const uint64_t *cf;
     const uint16_t *bucket;
@@ -85,7 +67,6 @@ struct W1Lds {
 };
 
 // Lane segment of nblk blocks starting at block b0 (RNG states positioned at draw b0).
-template <bool PACK>
 __device__ __forceinline__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s, const LogTab *__restrict__ lt, Rng &ri, Rng &rp,
                                uint32_t nblk, uint32_t b0, uint32_t phase, uint32_t lane, uint32_t r, uint32_t &flast,
                                uint32_t &nc, uint32_t &pick_err_blk, uint32_t &err)
@@ -101,7 +82,7 @@ __device__ __forceinline__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s
         tsum += Icur;
         bool slow = false;
         if (fcur < a.m) {
-            hist_add<PACK>(s.hist, fcur, 1u);
+            atomicAdd(&s.hist[fcur], 1u);
             slow = Inext <= thcur;
         } else if (pick_err_blk == WIDE_NONE) {
             pick_err_blk = b0 + b;
@@ -136,14 +117,14 @@ __device__ __forceinline__ uint64_t w1_segment(const WideArgs &a, const W1Lds &s
 }  // namespace
 
 // ---------------------------------------------------------------- W1
-// RUNS runs (waves) per workgroup share one copy of the pick tables in LDS (the host picks RUNS per network,
-// wide_w1_runs: the most resident waves the LDS allows); W1_WAVES is the resident waves per SIMD the register
-// budget is sized for. The LDS per workgroup ((m+1)*8 + 8 KiB tables + RUNS * 2m histograms) and the VGPRs
-// together set the occupancy.
+// RUNS runs (waves) per workgroup share one copy of the pick tables in LDS (the host picks RUNS per network
+// from the runtime's occupancy, wide_w1_runs); W1_WAVES is the resident waves per SIMD the register budget is
+// sized for. The LDS per workgroup ((m+1)*8 + 8 KiB tables + RUNS * 4m histograms) and the VGPRs together set
+// the occupancy.
 #ifndef W1_WAVES
 #define W1_WAVES 1
 #endif
-template <uint32_t RUNS, bool PACK>
+template <uint32_t RUNS>
 __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WAVES, 8))) void msim_wide_draws_kernel(const WideArgs a)
 {
     constexpr uint32_t W1_TPB = 64 * RUNS;
@@ -151,13 +132,12 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
     __shared__ LogTab s_log;
     __shared__ uint32_t s_cc[RUNS];
     const uint32_t m = a.m, tid = threadIdx.x;
-    const uint32_t hw = PACK ? (m + 1) / 2 : m;               // histogram words per run
     uint64_t *s_cf = sh64;                                    // [m + 1]
     uint16_t *s_bkt = (uint16_t *)(sh64 + m + 1);             // [WB_N]
-    uint32_t *s_hist = (uint32_t *)(s_bkt + WB_N);            // [RUNS][hw] (msim_wide: hist_add)
+    uint32_t *s_hist = (uint32_t *)(s_bkt + WB_N);            // [RUNS][m]
     for (uint32_t i = tid; i <= m; i += W1_TPB) s_cf[i] = a.cf[i];
     for (uint32_t i = tid; i < WB_N; i += W1_TPB) s_bkt[i] = a.bucket[i];
-    for (uint32_t i = tid; i < RUNS * hw; i += W1_TPB) s_hist[i] = 0;
+    for (uint32_t i = tid; i < RUNS * m; i += W1_TPB) s_hist[i] = 0;
     for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += W1_TPB) ((double *)&s_log)[i] = ((const double *)a.logt)[i];
     if (tid < RUNS) s_cc[tid] = 0;
     __syncthreads();
@@ -165,7 +145,7 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
     const uint32_t w = tid >> 6, lane = tid & 63u;
     const uint32_t r = blockIdx.x * RUNS + w;  // slice-local run
     if (r >= a.n) return;                   // wave-uniform; no block barrier below
-    const W1Lds s{s_cf, s_bkt, s_hist + w * hw, s_cc + w};
+    const W1Lds s{s_cf, s_bkt, s_hist + w * m, s_cc + w};
     const uint64_t run = a.run_begin + r;
     const Rng ri0 = rng_seed(seed_interval(a.seed_base, run));
     const Rng rp0 = rng_seed(seed_picker(a.seed_base, run));
@@ -184,7 +164,7 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
         const Rng ris = ri, rps = rp;
         uint32_t nc = 0;
         flast = fprev;
-        const uint64_t tsum = w1_segment<PACK>(a, s, &s_log, ri, rp, nblk, b0, ph, lane, r, flast, nc, pick_err_blk, err);
+        const uint64_t tsum = w1_segment(a, s, &s_log, ri, rp, nblk, b0, ph, lane, r, flast, nc, pick_err_blk, err);
         const uint64_t excl = wave_excl_scan(tsum, lane);
         const uint64_t t0 = Tph + excl, tend = t0 + tsum;
         lanes[(size_t)ph * 64 + lane] = WideLane{t0, nc, 0u};
@@ -201,7 +181,7 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
                 for (uint32_t b = 0; b < nblk; ++b) {
                     uint32_t th;
                     const uint32_t f = wide_pick(rng_next(p), s.cf, s.bucket, a.W, a.mult, th);
-                    if (f < m) hist_add<PACK>(s.hist, f, 0xFFFFFFFFu);
+                    if (f < m) atomicSub(&s.hist[f], 1u);
                 }
             } else if (lane == Ls) {
                 Rng i2 = ris, p2 = rps;
@@ -214,7 +194,7 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
                     const uint32_t f = wide_pick(rng_next(p2), s.cf, s.bucket, a.W, a.mult, th);
                     if ((int64_t)T >= D) {
                         if (ne == WIDE_NONE) ne = b0 + b;
-                        if (f < m) hist_add<PACK>(s.hist, f, 0xFFFFFFFFu);
+                        if (f < m) atomicSub(&s.hist[f], 1u);
                     } else {
                         lf = f;
                         tl = T;
@@ -262,7 +242,7 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
     for (int o = 32; o > 0; o >>= 1) err |= __shfl_xor(err, o, 64);
     wave_sync();
     uint32_t *hout = a.hist + (size_t)r * m;
-    for (uint32_t k = lane; k < m; k += 64) hout[k] = hist_get<PACK>(s.hist, k);
+    for (uint32_t k = lane; k < m; k += 64) hout[k] = s.hist[k];
     {  // this run's candidate slots on the dense W2 work list (one atomic per run)
         const uint32_t cc0 = *s.cc, ccn = cc0 < a.rcap ? cc0 : a.rcap;
         uint32_t base = 0;
@@ -487,28 +467,24 @@ __global__ void msim_wide_pick_kernel(const uint64_t *__restrict__ cf, const uin
 }
 
 // ---------------------------------------------------------------- host side
-size_t wide_w1_lds(uint32_t m, uint32_t runs, bool pack)
-{
-    return ((size_t)m + 1) * 8 + (size_t)WB_N * 2 + runs * (pack ? ((size_t)m + 1) / 2 : (size_t)m) * 4;
-}
+size_t wide_w1_lds(uint32_t m, uint32_t runs) { return ((size_t)m + 1) * 8 + (size_t)WB_N * 2 + runs * (size_t)m * 4; }
 // Runs per W1 workgroup: the most resident waves per CU (the runtime's occupancy of each instance at its
-// LDS, which counts its VGPRs too; ties: fewer runs per workgroup).
-template <uint32_t R, bool P>
+// LDS, which counts its VGPRs too; ties: fewer runs per workgroup). Measured on configs[4]
+// (profiles/r04/w1ab): 4 and 8 runs 9.17 ms, 2 runs 11.2 ms per W1 launch; W1 is issue-bound, so the
+// occupancy beyond 4 waves per SIMD gains nothing (a 16-bit packed histogram that allowed 5 was slower).
+template <uint32_t R>
 static size_t w1_waves_per_cu(uint32_t m)
 {
     int blocks = 0;
-    const size_t lds = wide_w1_lds(m, R, P);
+    const size_t lds = wide_w1_lds(m, R);
     if (lds > 150 * 1024 ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, msim_wide_draws_kernel<R, P>, 64 * R, lds) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, msim_wide_draws_kernel<R>, 64 * R, lds) != hipSuccess)
         return 0;
     return (size_t)blocks * R;
 }
-uint32_t wide_w1_runs(uint32_t m, bool pack)
+uint32_t wide_w1_runs(uint32_t m)
 {
-    const size_t w[4] = {pack ? w1_waves_per_cu<1, true>(m) : w1_waves_per_cu<1, false>(m),
-                         pack ? w1_waves_per_cu<2, true>(m) : w1_waves_per_cu<2, false>(m),
-                         pack ? w1_waves_per_cu<4, true>(m) : w1_waves_per_cu<4, false>(m),
-                         pack ? w1_waves_per_cu<8, true>(m) : w1_waves_per_cu<8, false>(m)};
+    const size_t w[4] = {w1_waves_per_cu<1>(m), w1_waves_per_cu<2>(m), w1_waves_per_cu<4>(m), w1_waves_per_cu<8>(m)};
     uint32_t best = 1;
     size_t bw = 0;
     for (int i = 0; i < 4; ++i)
@@ -516,8 +492,11 @@ uint32_t wide_w1_runs(uint32_t m, bool pack)
             bw = w[i];
             best = 1u << i;
         }
-    if (const char *e = getenv("MSIM_W1_RUNS")) best = (uint32_t)atoi(e);  // A/B override: 1, 2, 4 or 8
-    return best == 1 || best == 2 || best == 4 || best == 8 ? best : 4;
+    if (const char *e = getenv("MSIM_W1_RUNS")) {  // A/B override: 1, 2, 4 or 8 runs, when its LDS fits
+        const uint32_t r = (uint32_t)atoi(e);
+        if ((r == 1 || r == 2 || r == 4 || r == 8) && wide_w1_lds(m, r) <= 150 * 1024) best = r;
+    }
+    return best;
 }
 size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch)
 {
@@ -529,11 +508,10 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
 {
     static bool attr_done = false;
     if (!attr_done) {
-#define MSIM_W1_ATTR(R, P) \
-        (void)hipFuncSetAttribute((const void *)msim_wide_draws_kernel<R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-        MSIM_W1_ATTR(1, true) MSIM_W1_ATTR(2, true) MSIM_W1_ATTR(4, true) MSIM_W1_ATTR(8, true)
-        MSIM_W1_ATTR(1, false) MSIM_W1_ATTR(2, false) MSIM_W1_ATTR(4, false) MSIM_W1_ATTR(8, false)
-#undef MSIM_W1_ATTR
+        (void)hipFuncSetAttribute((const void *)msim_wide_draws_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        (void)hipFuncSetAttribute((const void *)msim_wide_draws_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        (void)hipFuncSetAttribute((const void *)msim_wide_draws_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        (void)hipFuncSetAttribute((const void *)msim_wide_draws_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
         (void)hipFuncSetAttribute((const void *)msim_wide_combine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr_done = true;
@@ -548,16 +526,9 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
     a.work = (uint32_t *)(ws + L.work_off);
     a.retry = (uint32_t *)(ws + L.retry_off);
     a.counts = (uint32_t *)(ws + L.counts_off);
-    // 16-bit histogram counts while a run cannot draw 2^16 blocks (every draw W1 makes is counted once)
-    bool pack = (uint64_t)a.B0 + 64ull * a.ST * a.nch + 64 < 65535ull;
-    if (const char *e = getenv("MSIM_W1_PACK")) pack = pack && atoi(e) != 0;  // A/B override
-    const uint32_t runs = wide_w1_runs(a.m, pack);
-    static bool told = false;
-    if (!told && getenv("MSIM_DEBUG")) {
-        fprintf(stderr, "msim: W1 runs/workgroup %u, packed histogram %d, LDS %zu B\n", runs, (int)pack, wide_w1_lds(a.m, runs, pack));
-        told = true;
-    }
-    const size_t l1 = wide_w1_lds(a.m, runs, pack), l3 = wide_w3_lds(a.m, a.rcap, a.nch);
+    const uint32_t runs = wide_w1_runs(a.m);
+    const size_t l1 = wide_w1_lds(a.m, runs), l3 = wide_w3_lds(a.m, a.rcap, a.nch);
+    if (l1 > 150 * 1024) return hipErrorInvalidValue;  // WIDE_MAX_M at one run per workgroup: 49 KiB
     if (l3 > 160 * 1024) return hipErrorInvalidValue;
     for (uint64_t off = 0; off < out.n_total; off += L.nr) {
         const uint32_t cn = (uint32_t)((out.n_total - off) < L.nr ? (out.n_total - off) : L.nr);
@@ -571,15 +542,11 @@ hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, con
         }
         if (hipMemsetAsync(a.counts, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return hipErrorUnknown;
         const dim3 g1((cn + runs - 1) / runs), b1(64 * runs);
-        switch (runs * 2 + (pack ? 1 : 0)) {
-        case 3: hipLaunchKernelGGL((msim_wide_draws_kernel<1, true>), g1, b1, l1, s, a); break;
-        case 5: hipLaunchKernelGGL((msim_wide_draws_kernel<2, true>), g1, b1, l1, s, a); break;
-        case 9: hipLaunchKernelGGL((msim_wide_draws_kernel<4, true>), g1, b1, l1, s, a); break;
-        case 17: hipLaunchKernelGGL((msim_wide_draws_kernel<8, true>), g1, b1, l1, s, a); break;
-        case 2: hipLaunchKernelGGL((msim_wide_draws_kernel<1, false>), g1, b1, l1, s, a); break;
-        case 4: hipLaunchKernelGGL((msim_wide_draws_kernel<2, false>), g1, b1, l1, s, a); break;
-        case 8: hipLaunchKernelGGL((msim_wide_draws_kernel<4, false>), g1, b1, l1, s, a); break;
-        default: hipLaunchKernelGGL((msim_wide_draws_kernel<8, false>), g1, b1, l1, s, a); break;
+        switch (runs) {
+        case 1: hipLaunchKernelGGL((msim_wide_draws_kernel<1>), g1, b1, l1, s, a); break;
+        case 2: hipLaunchKernelGGL((msim_wide_draws_kernel<2>), g1, b1, l1, s, a); break;
+        case 4: hipLaunchKernelGGL((msim_wide_draws_kernel<4>), g1, b1, l1, s, a); break;
+        default: hipLaunchKernelGGL((msim_wide_draws_kernel<8>), g1, b1, l1, s, a); break;
         }
         if (ee) (void)hipEventRecord(ee, s);
         // W2 grid: ~rho * blocks candidates per run, grid-stride beyond 16 384 workgroups

@@ -95,8 +95,8 @@ inline WideLayout wide_layout_for(double rho, uint32_t m, int64_t duration_ms, u
 }
 
 constexpr uint32_t W1_MAX_RUNS = 8;  // runs (waves) per W1 workgroup: 1, 2, 4 or 8, chosen per network
-size_t wide_w1_lds(uint32_t m, uint32_t runs, bool pack);
-uint32_t wide_w1_runs(uint32_t m, bool pack);
+size_t wide_w1_lds(uint32_t m, uint32_t runs);
+uint32_t wide_w1_runs(uint32_t m);
 size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch);
 // Runs out.n_total runs slice by slice (L.nr) on stream s; proto carries the tables and geometry.
 hipError_t launch_wide(const WideArgs &proto, const WideLayout &L, char *ws, const WideOut &out, hipStream_t s,

@@ -311,7 +311,7 @@ def timing_enable(on: bool = True) -> None:
 
 def timing_read() -> dict:
     """Summed draw-kernel / entity-engine / whole-launch milliseconds and the launch count since the last
-    enable/read (synchronises). draws_ms: K1 (honest pipeline) or D1 (entity engine); engine_ms: E1."""
+    enable/read (synchronises). draws_ms: K1 / W1 (honest pipelines; 0 for selfish networks); engine_ms: E1."""
     d, e, l, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
     check(lib.msim_timing_read_stages(ctypes.byref(d), ctypes.byref(e), ctypes.byref(l), ctypes.byref(n)),
           "msim_timing_read_stages")

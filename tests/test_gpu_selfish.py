@@ -199,22 +199,8 @@ def test_gpu_schedule_does_not_change_results(msim, monkeypatch, xth, no_macro):
     assert np.array_equal(base.best_height, other.best_height)
 
 
-@pytest.mark.parametrize("pool", ["1,0,1", "64,64,1000", "8,4,4", "2,48,2"])
-def test_gpu_pool_schedule_does_not_change_results(msim, oracle, monkeypatch, pool):
-    """E1's workgroup pool (msim_sel_kernels.hip sel_pool) only decides which lane steps which run's engine
-    episode and when: any queue threshold / refill floor / phase length gives the oracle's per-run counters
-    (configs[2], and a long-delay sweep corner where engine episodes are frequent)."""
-    monkeypatch.setenv("MSIM_SEL_POOL", pool)
-    for p, q, n in (([40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, 1024), ([49, 10, 12, 11, 8, 5, 3, 1, 1], [30000] * 9, 512)):
-        s = [1] + [0] * 8
-        res = _run(msim, p, q, s, n, begin=5)
-        f, st, _, _ = oracle.run_batch(p, q, s, D, n, 5, 1000, threads=16)
-        assert np.array_equal(res.found.astype(np.int64), f), pool
-        assert np.array_equal(res.stale.astype(np.int64), st), pool
-
-
 def test_gpu_selfish_eleven_miners_mixed_schedule(msim, oracle):
-    """Networks whose LDS does not fit the pool (11+ miners) keep the per-wave mixed schedule: vs the oracle."""
+    """An 11-miner network with one selfish miner (E1's mixed schedule at another miner count): vs the oracle."""
     p = [30, 14, 12, 11, 8, 5, 5, 5, 4, 3, 3]
     q = [1000] * 11
     s = [1] + [0] * 10

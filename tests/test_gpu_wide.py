@@ -171,3 +171,14 @@ def test_gpu_wide_sharding_is_exact(msim):
     for s_whole, s_halves in zip(whole.stats_total, msim.sums_to_stats(rows)):
         assert s_whole.blocks_share == s_halves.blocks_share
         assert s_whole.stale_rate == s_halves.stale_rate
+
+
+@pytest.mark.parametrize("runs", ["", "1", "2", "8"])
+def test_gpu_wide_max_network_any_runs_per_workgroup(msim, oracle, monkeypatch, runs):
+    """MSIM_MAX_WIDE_MINERS (4 096) miners: W1's runs per workgroup come from the runtime occupancy (or an
+    A/B override); every choice the library can make launches and gives the oracle's counters."""
+    if runs:
+        monkeypatch.setenv("MSIM_W1_RUNS", runs)
+    rnd = random.Random(4096)
+    w = [3000, 2000] + [rnd.randint(0, 3) for _ in range(4094)]
+    _vs_oracle(msim, oracle, w, [1000] * len(w), sum(w), 5 * DAY, 32)
