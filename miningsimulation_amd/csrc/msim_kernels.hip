@@ -161,8 +161,11 @@ __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int3
 // Three resident waves per SIMD (168 VGPRs, some spills at the episode's entry) rather than the two that 207
 // spill-free VGPRs allow: measured on MI355X (profiles/r03/k3ab), c2 with two overlapping streams 9.15M ->
 // 9.37M run-years/s, serial unchanged (K2 shares the GPU with the next step's K1 better).
+#ifndef MSIM_K2_WAVES
+#define MSIM_K2_WAVES 3
+#endif
 template <int M>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(3, 8))) void msim_episode_kernel(const SimParams p,
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_WAVES, 8))) void msim_episode_kernel(const SimParams p,
                                                                                                     const PipeArgs a)
 {
     const uint32_t cnt = *a.list_count;

@@ -39,6 +39,23 @@
 #ifndef SEL_HIT
 #define SEL_HIT(region)
 #endif
+// Engine-step section timing (diagnostic device builds only, -DSEL_ENGPROF=1): cycles per section of step(),
+// accumulated per lane in sel_engprof[] (the kernel prints them).
+#if defined(__HIP_DEVICE_COMPILE__) && defined(SEL_ENGPROF) && SEL_ENGPROF
+namespace msim {
+__device__ void sel_engprof_acc(int i, uint64_t c);
+}
+#define SEL_EP_DECL uint64_t ep_t = clock64()
+#define SEL_EP(i)                                      \
+    do {                                               \
+        const uint64_t ep_n = clock64();               \
+        sel_engprof_acc(i, ep_n - ep_t);               \
+        ep_t = ep_n;                                   \
+    } while (0)
+#else
+#define SEL_EP_DECL
+#define SEL_EP(i)
+#endif
 
 namespace msim {
 
@@ -821,6 +838,7 @@ struct Sel {
     {
         if (!(t_ < D && err == 0)) return false;  // main.cpp:150
         const int64_t t = t_;
+        SEL_EP_DECL;
         while (t == nbt_) {  // main.cpp:153-157
             SEL_HIT(0);
             if (kn_ >= (uint32_t)M) {
@@ -836,18 +854,25 @@ struct Sel {
             nbt_ += (int64_t)I;
         }
         if (err) return false;
+        SEL_EP(0);
         publish(env, t);
+        SEL_EP(1);
         const SelBest B = best(env);  // main.cpp:164
+        SEL_EP(2);
         notify(env, t, B);            // main.cpp:165-167
+        SEL_EP(3);
         merge(env);
         bpub = B.l;                   // main.cpp:171
         resolve(env);
+        SEL_EP(4);
         // Folding is a change of representation only, so a lane may fold before it is due: the device
         // folds every lane of a wave when any lane is due (one wave-uniform branch, and lanes that folded
         // together are due again later, together).
         const bool due = fold_due(env, B.l);
         if (env.fold_vote(due)) fold(env, due);
+        SEL_EP(5);
         t_ = lmin(nbt_, earliest(env, t));  // main.cpp:176-182
+        SEL_EP(6);
         return true;
     }
     // main.cpp:185-189: BestChain at the end of the run, no notify.

@@ -10,6 +10,15 @@
 
 namespace msim {
 
+#if SEL_ENGPROF
+// per-lane section cycles of the engine step (msim_sel.h SEL_EP), printed by E1 for a few waves
+__device__ uint64_t sel_engprof_buf[8][TPB];
+__device__ void sel_engprof_acc(int i, uint64_t c)
+{
+    sel_engprof_buf[i][threadIdx.x] += blockIdx.x == 0 ? c : 0;  // block 0 only (others would race)
+}
+#endif
+
 #ifndef SEL_WAVES
 #define SEL_WAVES 2  // E1 occupancy target (waves per SIMD): 256 VGPRs, no spills
 #endif
@@ -185,6 +194,9 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #ifndef SEL_PROF
 #define SEL_PROF 0
 #endif
+#ifndef SEL_ENGPROF
+#define SEL_ENGPROF 0
+#endif
 #ifndef SEL_MSTEPS
 #define SEL_MSTEPS 2
 #endif
@@ -223,7 +235,7 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
         park(r);
         mode = 3;
     }
-#if SEL_PROF  // per-wave phase timing (diagnostic builds only: scripts/build_sel_variant.sh prof -DSEL_PROF=1)
+#if SEL_PROF  // per-wave phase timing (diagnostic builds only: scripts/build_variant.sh prof msim_sel_kernels.hip -DSEL_PROF=1)
     uint64_t pt_m = 0, pt_e = 0, pn_m = 0, pn_e = 0, pi_m = 0, pi_e = 0, pl_m = 0, pl_e = 0;
     const uint64_t pt0 = clock64();
 #endif
@@ -432,6 +444,17 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         }
     }
     block_reduce_store<M>(v, a.partials + ((size_t)point * a.wpp + a.s0 / TPB + blk) * 6 * M);
+#if SEL_ENGPROF
+    if (blockIdx.x == 0 && (tid & 63u) == 0u) {
+        unsigned long long t[7];
+        for (int i = 0; i < 7; ++i) {
+            t[i] = 0;
+            for (uint32_t l = tid; l < tid + 64; ++l) t[i] += sel_engprof_buf[i][l];
+        }
+        printf("ENGPROF wave %u finds %llu publish %llu best %llu notify %llu merge+resolve %llu fold %llu earliest %llu\n",
+               tid / 64u, t[0], t[1], t[2], t[3], t[4], t[5], t[6]);
+    }
+#endif
 }
 
 // E2: one lane per flagged (point, run), wide capacities, draws from the seeds.

@@ -85,4 +85,49 @@ uint32_t gen_run(const uint64_t *weights, const int64_t *props, const uint8_t *s
     *base = o.base;
     return 0;
 }
+
+// test.cpp:213-367 TestSelfishStrategy on G's state machine: one selfish miner (miner 0 of the store) with a
+// hand-built chain, then FoundBlock (op 0: t, best_chain_size) or NotifyBestChain (op 1: the best chain held
+// by miner 1 of the store, t). Owners are the KAT's miner ids (G stores an id class; here the class of the
+// selfish miner is its id). Returns the resulting chain length (out arrays of cap entries).
+uint32_t gen_kat(uint32_t sid, int64_t prop, int op, int64_t t, uint32_t bcs, const uint32_t *own, const int64_t *arr,
+                 uint32_t n, const uint32_t *bown, const int64_t *barr, uint32_t bn, uint32_t *out_own, int64_t *out_arr,
+                 uint32_t cap)
+{
+    const uint32_t wcap = 4096;
+    uint64_t cum[2] = {50, 100};
+    int64_t props[2] = {prop, prop};
+    uint8_t self[2] = {1, 0};
+    uint32_t cls[2] = {sid, 0xFFFFFFFEu};
+    GenParams g;
+    memset(&g, 0, sizeof(g));
+    g.duration_ms = 1;
+    g.mult = 0xFFFFFFFFFFFFFFFFull / 100;
+    g.m = 2;
+    g.umax = GEN_GENESIS;
+    g.cum = cum;
+    g.prop = props;
+    g.self = self;
+    g.cls = cls;
+    HostStore s(2, wcap);
+    for (uint32_t i = 0; i < n; ++i) s.put(0, i, own[i], arr[i]);
+    s.set_size(0, n);
+    for (uint32_t i = 0; i < bn; ++i) s.put(1, i, bown[i], barr[i]);
+    s.set_size(1, bn);
+    Gen<HostStore> e(s, g);
+    e.bcs = (int32_t)bcs;
+    e.now = t;
+    if (op == 0) {
+        e.found_block(0, t);
+    } else {
+        e.selfish_reveal(0, bn, t);  // simulation.h:177-180: reveal, then reorg
+        e.reorg(0, 1, bn);
+    }
+    const uint32_t m = s.size(0);
+    for (uint32_t i = 0; i < m && i < cap; ++i) {
+        out_own[i] = s.own(0, i);
+        out_arr[i] = s.arr(0, i);
+    }
+    return m;
+}
 }

@@ -156,3 +156,39 @@ def test_single_miner_zero_delay_fold(gen, oracle):
     _check_batch(gen, oracle, [100], [0], [False], 10 * DAY, 4, 17, cap=16)
     # a lone selfish miner never publishes (its lead never drops), so nothing folds: the window holds the run
     _check_batch(gen, oracle, [100], [0], [True], 10 * DAY, 4, 17, cap=4096)
+
+
+def test_selfish_strategy_kats_on_general_engine(native_tests):
+    """The reference's only asserting test, test.cpp:213-367 TestSelfishStrategy, replayed on the PRODUCT's
+    general engine (msim_general.h: FoundBlock, MaybeSelfishReveal, MaybeReorg on explicit chains), not only on
+    the oracle: every case's resulting chain equals the reference's expected chain."""
+    import json
+    import os
+
+    lib = ctypes.CDLL(native_tests["general_host"])
+    u32p, i64p = ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int64)
+    lib.gen_kat.restype = ctypes.c_uint32
+    lib.gen_kat.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, u32p, i64p,
+                            ctypes.c_uint32, u32p, i64p, ctypes.c_uint32, u32p, i64p, ctypes.c_uint32]
+    doc = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "selfish_strategy_kats.json")))
+    W = (1 << 63) - 1
+
+    def chain(c):
+        return [(0xFFFFFFFF, 0) if b == "G" else (b[0], W if b[1] == "W" else b[1]) for b in c]
+
+    def arrays(c):
+        n = max(len(c), 1)
+        return (ctypes.c_uint32 * n)(*[b[0] for b in c]), (ctypes.c_int64 * n)(*[b[1] for b in c]), len(c)
+
+    sm = doc["selfish_miner"]
+    for case in doc["cases"]:
+        own, arr, n = arrays(chain(case["chain"]))
+        op = case["op"]
+        if op[0] == "found":
+            code, t, bcs, best = 0, op[1], op[2], []
+        else:
+            code, t, bcs, best = 1, op[2], 0, chain(op[1])
+        bown, barr, bn = arrays(best)
+        oo, oa = (ctypes.c_uint32 * 4096)(), (ctypes.c_int64 * 4096)()
+        m = lib.gen_kat(sm["id"], sm["propagation_ms"], code, t, bcs, own, arr, n, bown, barr, bn, oo, oa, 4096)
+        assert [(oo[i], oa[i]) for i in range(m)] == chain(case["expect"]), case["name"]
