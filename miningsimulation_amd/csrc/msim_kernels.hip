@@ -168,9 +168,19 @@ template <int M>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_WAVES, 8))) void msim_episode_kernel(const SimParams p,
                                                                                                     const PipeArgs a)
 {
+    // the draw tables in LDS: an episode's draws read them in its dependent chain (global: ~600-900 cycles
+    // per read, LDS: ~50)
+    __shared__ LogTab s_log;
+    __shared__ PickTab s_pick;
+    for (uint32_t i = threadIdx.x; i < sizeof(LogTab) / 8; i += TPB) ((double *)&s_log)[i] = ((const double *)a.tab.logt)[i];
+    for (uint32_t i = threadIdx.x; i < sizeof(PickTab) / 4; i += TPB) ((uint32_t *)&s_pick)[i] = ((const uint32_t *)a.tab.pick)[i];
+    __syncthreads();
+    PipeArgs la = a;
+    la.tab.logt = &s_log;
+    la.tab.pick = &s_pick;
     const uint32_t cnt = *a.list_count;
     const uint32_t lim = cnt < a.lcap ? cnt : a.lcap;
-    for (uint32_t idx = blockIdx.x * TPB + threadIdx.x; idx < lim; idx += gridDim.x * TPB) episode_entry<M>(p, a, idx);
+    for (uint32_t idx = blockIdx.x * TPB + threadIdx.x; idx < lim; idx += gridDim.x * TPB) episode_entry<M>(p, la, idx);
 }
 
 // K3: one lane per run (msim_pipeline.h combine_run), then the MinerStats reduction.
@@ -181,11 +191,19 @@ __global__ __launch_bounds__(TPB) void msim_combine_kernel(const SimParams p, co
                                                           uint32_t *__restrict__ err_count, uint32_t *__restrict__ err_list,
                                                           const uint32_t err_cap)
 {
-    __shared__ uint32_t s_ns[K3_SEG_MAX][TPB];  // per-lane list counts of the run's segments (combine_run)
+    __shared__ uint32_t s_ns[K3_SCRATCH][TPB];  // per-lane scratch of combine_run (segment counts, episodes)
+    __shared__ LogTab s_log;                    // the draw tables for the end group's redraw (as K2)
+    __shared__ PickTab s_pick;
+    for (uint32_t i = threadIdx.x; i < sizeof(LogTab) / 8; i += TPB) ((double *)&s_log)[i] = ((const double *)a.tab.logt)[i];
+    for (uint32_t i = threadIdx.x; i < sizeof(PickTab) / 4; i += TPB) ((uint32_t *)&s_pick)[i] = ((const uint32_t *)a.tab.pick)[i];
+    __syncthreads();
+    PipeArgs la = a;
+    la.tab.logt = &s_log;
+    la.tab.pick = &s_pick;
     const uint32_t r = blockIdx.x * TPB + threadIdx.x;
     const bool active = r < n;
     uint32_t F[M], S[M];
-    const bool ok = active ? combine_run<M>(p, a, r, F, S, &s_ns[0][threadIdx.x], TPB) : false;
+    const bool ok = active ? combine_run<M>(p, la, r, F, S, &s_ns[0][threadIdx.x], TPB) : false;
     uint64_t v[6 * M];
 #pragma unroll
     for (int i = 0; i < 6 * M; ++i) v[i] = 0;

@@ -359,13 +359,16 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 // combine_run for the first lane of a few workgroups.
 #if defined(__HIP_DEVICE_COMPILE__) && defined(K3_PROF) && K3_PROF
 #define K3T(i) k3t[i] = clock64()
-#define K3T_DECL uint64_t k3t[8] = {0, 0, 0, 0, 0, 0, 0, 0}; K3T(0)
+#define K3T_DECL uint64_t k3t[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; K3T(0)
 #define K3T_PRINT                                                                                               \
     if (threadIdx.x == 0 && blockIdx.x % 16 == 0)                                                               \
-        printf("K3PROF blk %u seg %llu segcnt %llu groups %llu redraw %llu prevgrp %llu eps %llu\n", blockIdx.x, \
+        printf("K3PROF blk %u seg %llu segcnt %llu groups %llu redraw %llu prevgrp %llu eps %llu | nslow %llu idx %llu hdr %llu chain %llu apply %llu\n", blockIdx.x, \
                (unsigned long long)(k3t[1] - k3t[0]), (unsigned long long)(k3t[2] - k3t[1]),                    \
                (unsigned long long)(k3t[3] - k3t[2]), (unsigned long long)(k3t[4] - k3t[3]),                    \
-               (unsigned long long)(k3t[5] - k3t[4]), (unsigned long long)(k3t[6] - k3t[5]))
+               (unsigned long long)(k3t[5] - k3t[4]), (unsigned long long)(k3t[6] - k3t[5]),                    \
+               (unsigned long long)(k3t[7] - k3t[5]), (unsigned long long)(k3t[8] - k3t[7]),                    \
+               (unsigned long long)(k3t[9] - k3t[8]), (unsigned long long)(k3t[10] - k3t[9]),                   \
+               (unsigned long long)(k3t[6] - k3t[10]))
 #else
 #define K3T(i)
 #define K3T_DECL
@@ -373,8 +376,9 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 #endif
 
 // Combine one run r of a slice. Returns false when the run must be recomputed by the retry path.
-// nsw: K3_SEG_MAX words of per-run scratch at stride nss (device: the lane's LDS column).
-constexpr uint32_t K3_SEG_MAX = 32;
+// nsw: K3_SCRATCH words of per-run scratch at stride nss (device: the lane's LDS column): the list counts of
+// the run's segments, then the record indices of the episodes that apply.
+constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = 32, K3_SCRATCH = K3_SEG_MAX + K3_EP_MAX;
 template <int M>
 MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M],
                          uint32_t *nsw, size_t nss)
@@ -394,7 +398,10 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     for (uint32_t j0 = 0; j0 < a.nseg && e < 0; j0 += KB) {
         uint64_t ss[KB];
 #pragma unroll
-        for (uint32_t j = 0; j < KB; ++j) ss[j] = j0 + j < a.nseg ? a.segsum[(size_t)(j0 + j) * a.nr + r] : 0ull;
+        for (uint32_t j = 0; j < KB; ++j) {  // unconditional (clamped) loads: all KB in flight together
+            const uint32_t jj = j0 + j < a.nseg ? j0 + j : a.nseg - 1;
+            ss[j] = a.segsum[(size_t)jj * a.nr + r];
+        }
 #pragma unroll
         for (uint32_t j = 0; j < KB; ++j) {
             if (e < 0 && j0 + j < a.nseg) {
@@ -411,12 +418,16 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         for (int j0 = 0; j0 < e; j0 += (int)KB) {
             uint32_t c[KB][CNT_WORDS];
 #pragma unroll
-            for (uint32_t j = 0; j < KB; ++j)
+            for (uint32_t j = 0; j < KB; ++j) {
+                const int jj = j0 + (int)j < e ? j0 + (int)j : e - 1;  // clamped: unconditional loads, masked below
 #pragma unroll
-                for (uint32_t w = 0; w < CNT_WORDS; ++w)
-                    c[j][w] = (j0 + (int)j < e && (w < (uint32_t)(M + 1) / 2 || w == CNT_WORDS - 1))
-                                  ? a.segcnt[((size_t)(j0 + (int)j) * CNT_WORDS + w) * a.nr + r]
-                                  : 0u;
+                for (uint32_t w = 0; w < CNT_WORDS; ++w) {
+                    const uint32_t v = (w < (uint32_t)(M + 1) / 2 || w == CNT_WORDS - 1)
+                                           ? a.segcnt[((size_t)jj * CNT_WORDS + w) * a.nr + r]
+                                           : 0u;
+                    c[j][w] = j0 + (int)j < e ? v : 0u;
+                }
+            }
 #pragma unroll
             for (uint32_t j = 0; j < KB; ++j) {
 #pragma unroll
@@ -438,7 +449,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     for (uint32_t g0 = 0; g0 < a.gps && G == a.gps; g0 += KG) {
         uint32_t gs[KG];
 #pragma unroll
-        for (uint32_t g = 0; g < KG; ++g) gs[g] = g0 + g < a.gps ? a.gsum[(gb + g0 + g) * a.nr + r] : 0u;
+        for (uint32_t g = 0; g < KG; ++g) gs[g] = a.gsum[(gb + (g0 + g < a.gps ? g0 + g : a.gps - 1)) * a.nr + r];
 #pragma unroll
         for (uint32_t g = 0; g < KG; ++g) {
             if (G == a.gps && g0 + g < a.gps) {
@@ -494,13 +505,16 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     // configs[1]) takes the same walk one read at a time.
     K3T(5);
     uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
-    constexpr uint32_t EP_MAX = 32, SEG_MAX = K3_SEG_MAX;
+    constexpr uint32_t EP_MAX = K3_EP_MAX, SEG_MAX = K3_SEG_MAX;
     uint32_t tot = 0;
     const bool fits = (uint32_t)e < SEG_MAX;
     if (fits) {
         uint32_t nsv[SEG_MAX];
 #pragma unroll
-        for (uint32_t j = 0; j < SEG_MAX; ++j) nsv[j] = j <= (uint32_t)e ? a.nslow[(size_t)j * a.nr + r] : 0u;
+        for (uint32_t j = 0; j < SEG_MAX; ++j) {
+            const uint32_t v = a.nslow[(size_t)(j <= (uint32_t)e ? j : (uint32_t)e) * a.nr + r];
+            nsv[j] = j <= (uint32_t)e ? v : 0u;
+        }
 #pragma unroll
         for (uint32_t j = 0; j < SEG_MAX; ++j) {
             if (nsv[j] > a.cap) return false;
@@ -508,6 +522,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             nsw[j * nss] = nsv[j];  // read back below at data-dependent positions
         }
     }
+    K3T(7);
     if (fits && tot <= EP_MAX) {
         uint32_t idx[EP_MAX];
         {
@@ -527,6 +542,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
                 idx[t] = v;
             }
         }
+        K3T(8);
         uint32_t st[EP_MAX], en[EP_MAX], fl[EP_MAX];
 #pragma unroll
         for (uint32_t t = 0; t < EP_MAX; ++t) {
@@ -539,7 +555,11 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
                 fl[t] = rec[1];
             }
         }
+        K3T(9);
+        // which episodes apply: the chain over the headers alone (registers); their record indices go to the
+        // lane's scratch column so that the deltas are then loaded APPLY_B episodes at a time
         bool stop = false;
+        uint32_t na = 0;
 #pragma unroll
         for (uint32_t t = 0; t < EP_MAX; ++t) {
             if (stop || t >= tot) continue;
@@ -549,17 +569,32 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             }
             if (st[t] < cursor) continue;  // consumed by the previous episode
             if (fl[t] & (REC_ERR | REC_SKIP)) return false;
-            const uint32_t *rec = a.recs + (size_t)idx[t] * a.rec_words;
-#pragma unroll
-            for (int k = 0; k < M; ++k) {
-                F[k] += rec[2 + k];
-                S[k] += rec[2 + M + k];
-            }
+            nsw[(SEG_MAX + na) * nss] = idx[t];
+            ++na;
             cursor = en[t];
             if (fl[t] & REC_ENDED) {  // the run ended inside this episode
                 cursor = 0xFFFFFFFFu;
                 stop = true;
             }
+        }
+        K3T(10);
+        constexpr uint32_t APPLY_B = 4;
+        for (uint32_t t0 = 0; t0 < na; t0 += APPLY_B) {
+            uint32_t d[APPLY_B][2 * M];
+#pragma unroll
+            for (uint32_t b = 0; b < APPLY_B; ++b) {
+                const uint32_t t = t0 + b < na ? t0 + b : na - 1;  // clamped: unconditional loads, masked below
+                const uint32_t *rec = a.recs + (size_t)nsw[(SEG_MAX + t) * nss] * a.rec_words;
+#pragma unroll
+                for (int k = 0; k < 2 * M; ++k) d[b][k] = rec[2 + k];
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < APPLY_B; ++b)
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    F[k] += t0 + b < na ? d[b][k] : 0u;
+                    S[k] += t0 + b < na ? d[b][M + k] : 0u;
+                }
         }
     } else {
         bool stop = false;
@@ -622,9 +657,9 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     for (uint32_t j0 = 0; j0 < seg; j0 += 8) {
         uint64_t ss[8];
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) ss[j] = j0 + j < seg ? a.segsum[(size_t)(j0 + j) * a.nr + e.run] : 0ull;
+        for (uint32_t j = 0; j < 8; ++j) ss[j] = a.segsum[(size_t)(j0 + j < seg ? j0 + j : seg - 1) * a.nr + e.run];
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) T += (int64_t)ss[j];
+        for (uint32_t j = 0; j < 8; ++j) T += j0 + j < seg ? (int64_t)ss[j] : 0;  // clamped loads, masked
     }
     if (T >= p.duration_ms) {  // beyond the end of the run: never applied
         rec[1] = REC_SKIP;

@@ -127,7 +127,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     for (uint32_t i = 0; i < count; ++i) episode_entry<M>(p, a, i);
     for (uint32_t r = 0; r < n; ++r) {
         uint32_t F[M], S[M];
-        uint32_t nsw[K3_SEG_MAX];
+        uint32_t nsw[K3_SCRATCH];
         ok[r] = combine_run<M>(p, a, r, F, S, nsw, 1) ? 1 : 0;
         for (int k = 0; k < M; ++k) {
             found[(size_t)r * M + k] = F[k];
