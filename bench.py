@@ -35,20 +35,20 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 
 
 # PMC constants of the dominant kernel per launch at the default run counts, from rocprofv3 --pmc passes of
-# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc_r04.sh: FETCH_SIZE, WRITE_SIZE and the
-# SQ set in separate passes; files under profiles/r04/pmc/, values there summed over 2 launches, KB). PMC counters
+# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_r04_final.sh: FETCH_SIZE, WRITE_SIZE and the
+# SQ set in separate passes; files under profiles/r04/final/pmc/, values there summed over 2 launches, KB). PMC counters
 # cannot be collected inside the timed process: these are the recorded values of the same kernel.
 #   traffic = FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of wide reads, MI355X_MICROARCH.md §HBM)
 #             + WRITE_SIZE, bytes per launch;
 #   valu    = SQ_INSTS_VALU (wave instructions) per launch: the counter-based VALU issue fraction is
 #             valu x 64 lanes / the kernel's live time / peak, reported beside the SURVEY 8(d) convention.
 PMC = {
-    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "fetch_kb": 21265.6 / 2, "write_kb": 883911 / 2,
-                    "valu": 3.55634e9 / 2, "src": "profiles/r04/pmc/pmc_c2.txt"},
-    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "fetch_kb": 9.40858e6 / 2,
-                     "write_kb": 4.6686e7 / 2, "valu": 4.99608e10 / 2, "src": "profiles/r04/pmc/pmc_c3.txt"},
-    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "fetch_kb": 3309 / 2, "write_kb": 1.82864e6 / 2,
-                    "valu": 1.07196e10 / 2, "src": "profiles/r04/pmc/pmc_c5.txt"},
+    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "fetch_kb": 22179.9 / 2, "write_kb": 886677 / 2,
+                    "valu": 3.55634e9 / 2, "src": "profiles/r04/final/pmc/pmc_c2.txt"},
+    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "fetch_kb": 9.42627e6 / 2,
+                     "write_kb": 4.66685e7 / 2, "valu": 4.99608e10 / 2, "src": "profiles/r04/final/pmc/pmc_c3.txt"},
+    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "fetch_kb": 3266.38 / 2, "write_kb": 1.82867e6 / 2,
+                    "valu": 1.07196e10 / 2, "src": "profiles/r04/final/pmc/pmc_c5.txt"},
 }
 # rocprofv3 --kernel-trace --stats summaries of the exact bench commands (default streams and --streams 1), whose
 # average duration of the dominant kernel is the file-backed counterpart of the live HIP-event time in the line.

@@ -164,7 +164,8 @@ hipError_t launch_sel_finalize(const uint64_t *partials, uint32_t n_points, uint
 
 size_t partials_words(uint32_t m, uint32_t n, uint32_t err_cap)
 {
-    const size_t nb = (n + TPB - 1) / TPB, nbr = (err_cap + TPB - 1) / TPB;
+    // one row per 64 runs: the pipeline's combine kernel K3 runs one-wave workgroups (msim_kernels.hip)
+    const size_t nb = (n + 63) / 64, nbr = (err_cap + TPB - 1) / TPB;
     return (nb + nbr) * 6 * (size_t)m;
 }
 

@@ -164,46 +164,56 @@ __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int3
 #ifndef MSIM_K2_WAVES
 #define MSIM_K2_WAVES 3
 #endif
+// Workgroup sizes of K2 and K3. K3 has one lane per run, so a 256-lane workgroup put the 32 768 runs of a c2
+// slice on 128 workgroups, half the CUs; one-wave workgroups spread them over all 256.
+#ifndef MSIM_K2_TPB
+#define MSIM_K2_TPB 256
+#endif
+#ifndef MSIM_K3_TPB
+#define MSIM_K3_TPB 64
+#endif
+constexpr int K2_TPB = MSIM_K2_TPB, K3_TPB = MSIM_K3_TPB;
+static_assert(K3_TPB % 64 == 0 && K3_TPB <= TPB && TPB % K3_TPB == 0, "K3 workgroups: whole waves, dividing TPB");
 template <int M>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_WAVES, 8))) void msim_episode_kernel(const SimParams p,
+__global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_WAVES, 8))) void msim_episode_kernel(const SimParams p,
                                                                                                     const PipeArgs a)
 {
     // the draw tables in LDS: an episode's draws read them in its dependent chain (global: ~600-900 cycles
     // per read, LDS: ~50)
     __shared__ LogTab s_log;
     __shared__ PickTab s_pick;
-    for (uint32_t i = threadIdx.x; i < sizeof(LogTab) / 8; i += TPB) ((double *)&s_log)[i] = ((const double *)a.tab.logt)[i];
-    for (uint32_t i = threadIdx.x; i < sizeof(PickTab) / 4; i += TPB) ((uint32_t *)&s_pick)[i] = ((const uint32_t *)a.tab.pick)[i];
+    for (uint32_t i = threadIdx.x; i < sizeof(LogTab) / 8; i += K2_TPB) ((double *)&s_log)[i] = ((const double *)a.tab.logt)[i];
+    for (uint32_t i = threadIdx.x; i < sizeof(PickTab) / 4; i += K2_TPB) ((uint32_t *)&s_pick)[i] = ((const uint32_t *)a.tab.pick)[i];
     __syncthreads();
     PipeArgs la = a;
     la.tab.logt = &s_log;
     la.tab.pick = &s_pick;
     const uint32_t cnt = *a.list_count;
     const uint32_t lim = cnt < a.lcap ? cnt : a.lcap;
-    for (uint32_t idx = blockIdx.x * TPB + threadIdx.x; idx < lim; idx += gridDim.x * TPB) episode_entry<M>(p, la, idx);
+    for (uint32_t idx = blockIdx.x * K2_TPB + threadIdx.x; idx < lim; idx += gridDim.x * K2_TPB) episode_entry<M>(p, la, idx);
 }
 
 // K3: one lane per run (msim_pipeline.h combine_run), then the MinerStats reduction.
 template <int M>
-__global__ __launch_bounds__(TPB) void msim_combine_kernel(const SimParams p, const PipeArgs a, const uint32_t n,
+__global__ __launch_bounds__(K3_TPB) void msim_combine_kernel(const SimParams p, const PipeArgs a, const uint32_t n,
                                                           const uint32_t rel_begin, uint64_t *__restrict__ partials,
                                                           uint32_t *__restrict__ records, uint32_t *__restrict__ best_h,
                                                           uint32_t *__restrict__ err_count, uint32_t *__restrict__ err_list,
                                                           const uint32_t err_cap)
 {
-    __shared__ uint32_t s_ns[K3_SCRATCH][TPB];  // per-lane scratch of combine_run (segment counts, episodes)
-    __shared__ LogTab s_log;                    // the draw tables for the end group's redraw (as K2)
+    __shared__ uint32_t s_ns[K3_SCRATCH][K3_TPB];  // per-lane scratch of combine_run (segment counts, episodes)
+    __shared__ LogTab s_log;                       // the draw tables for the end group's redraw (as K2)
     __shared__ PickTab s_pick;
-    for (uint32_t i = threadIdx.x; i < sizeof(LogTab) / 8; i += TPB) ((double *)&s_log)[i] = ((const double *)a.tab.logt)[i];
-    for (uint32_t i = threadIdx.x; i < sizeof(PickTab) / 4; i += TPB) ((uint32_t *)&s_pick)[i] = ((const uint32_t *)a.tab.pick)[i];
+    for (uint32_t i = threadIdx.x; i < sizeof(LogTab) / 8; i += K3_TPB) ((double *)&s_log)[i] = ((const double *)a.tab.logt)[i];
+    for (uint32_t i = threadIdx.x; i < sizeof(PickTab) / 4; i += K3_TPB) ((uint32_t *)&s_pick)[i] = ((const uint32_t *)a.tab.pick)[i];
     __syncthreads();
     PipeArgs la = a;
     la.tab.logt = &s_log;
     la.tab.pick = &s_pick;
-    const uint32_t r = blockIdx.x * TPB + threadIdx.x;
+    const uint32_t r = blockIdx.x * K3_TPB + threadIdx.x;
     const bool active = r < n;
     uint32_t F[M], S[M];
-    const bool ok = active ? combine_run<M>(p, la, r, F, S, &s_ns[0][threadIdx.x], TPB) : false;
+    const bool ok = active ? combine_run<M>(p, la, r, F, S, &s_ns[0][threadIdx.x], K3_TPB) : false;
     uint64_t v[6 * M];
 #pragma unroll
     for (int i = 0; i < 6 * M; ++i) v[i] = 0;
@@ -237,7 +247,7 @@ __global__ __launch_bounds__(TPB) void msim_combine_kernel(const SimParams p, co
         }
         if (best_h) best_h[rel] = L;
     }
-    block_reduce_store<M>(v, partials + (size_t)blockIdx.x * 6 * M);
+    block_reduce_store<M, K3_TPB>(v, partials + (size_t)blockIdx.x * 6 * M);
 }
 
 // ------------------------------------------------------------------ host-side launch table
@@ -300,8 +310,8 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.grec = (GroupRec *)(ws + L.grec_off);
     da.list = (EpEntry *)(ws + L.list_off);
     da.list_count = (uint32_t *)(ws + L.count_off);
-    uint32_t ep_grid = (L.lcap + TPB - 1) / TPB;
-    if (ep_grid > 8192) ep_grid = 8192;
+    uint32_t ep_grid = (L.lcap + K2_TPB - 1) / K2_TPB;
+    if (ep_grid > 8192u * (TPB / K2_TPB)) ep_grid = 8192u * (TPB / K2_TPB);
     if (ep_grid == 0) ep_grid = 1;
     for (uint32_t off = 0; off < a.n; off += L.nr) {
         const uint32_t cn = (a.n - off) < L.nr ? (a.n - off) : L.nr;
@@ -317,9 +327,9 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
         hipError_t e = launch_draws(da, a.stream);
         if (ee) (void)hipEventRecord(ee, a.stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((msim_episode_kernel<M>), dim3(ep_grid), dim3(TPB), 0, a.stream, a.p, pa);
-        hipLaunchKernelGGL((msim_combine_kernel<M>), dim3((cn + TPB - 1) / TPB), dim3(TPB), 0, a.stream, a.p, pa, cn,
-                           off, parts + (size_t)(off / TPB) * 6 * M, a.records, a.best_h, a.err_count, a.err_list,
+        hipLaunchKernelGGL((msim_episode_kernel<M>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
+        hipLaunchKernelGGL((msim_combine_kernel<M>), dim3((cn + K3_TPB - 1) / K3_TPB), dim3(K3_TPB), 0, a.stream, a.p, pa,
+                           cn, off, parts + (size_t)(off / K3_TPB) * 6 * M, a.records, a.best_h, a.err_count, a.err_list,
                            a.err_cap);
     }
     return hipGetLastError();
@@ -330,9 +340,10 @@ static hipError_t launch_m(const LaunchArgs &a)
 {
     const uint32_t nb = (a.n + TPB - 1) / TPB;
     const uint32_t nbr = (a.err_cap + TPB - 1) / TPB;
+    const uint32_t nrow = a.pl ? (a.n + K3_TPB - 1) / K3_TPB : nb;  // partial rows: one per workgroup
     const bool self = a.p.selfish >= 0;
     uint64_t *parts = a.partials;
-    uint64_t *parts_retry = a.partials + (size_t)nb * 6 * M;
+    uint64_t *parts_retry = a.partials + (size_t)nrow * 6 * M;
     if (a.pl) {
         const hipError_t e = launch_pipeline<M>(a, parts);
         if (e != hipSuccess) return e;
@@ -351,7 +362,7 @@ static hipError_t launch_m(const LaunchArgs &a)
     launch_retry<M>(a, parts_retry, nbr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_finalize(a.partials, nb + nbr, (uint32_t)(6 * M), a.sums, a.err_count, a.fail_count, a.err_cap,
+    return launch_finalize(a.partials, nrow + nbr, (uint32_t)(6 * M), a.sums, a.err_count, a.fail_count, a.err_cap,
                            a.status, a.stream);
 }
 

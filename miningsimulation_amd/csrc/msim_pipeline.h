@@ -33,6 +33,9 @@ namespace msim {
 #ifndef MSIM_K2_NX
 #define MSIM_K2_NX NX_FAST  // K2's extra in-flight blocks (measured: NX_WIDE 150 us vs NX_FAST 141 us per c2 launch)
 #endif
+#ifndef MSIM_K2_DEEP
+#define MSIM_K2_DEEP 1  // K2 follows forks deeper than the 16-height window (else such episodes flag their run)
+#endif
 constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
 constexpr uint32_t MIN_SEG = 512;       // shortest K1 worker (keeps the jump-ahead cost < 5 %)
 constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pairs (<= 16 owners)
@@ -359,16 +362,14 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 // combine_run for the first lane of a few workgroups.
 #if defined(__HIP_DEVICE_COMPILE__) && defined(K3_PROF) && K3_PROF
 #define K3T(i) k3t[i] = clock64()
-#define K3T_DECL uint64_t k3t[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; K3T(0)
+#define K3T_DECL uint64_t k3t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; K3T(0)
 #define K3T_PRINT                                                                                               \
     if (threadIdx.x == 0 && blockIdx.x % 16 == 0)                                                               \
-        printf("K3PROF blk %u seg %llu segcnt %llu groups %llu redraw %llu prevgrp %llu eps %llu | nslow %llu idx %llu hdr %llu chain %llu apply %llu\n", blockIdx.x, \
-               (unsigned long long)(k3t[1] - k3t[0]), (unsigned long long)(k3t[2] - k3t[1]),                    \
+        printf("K3PROF blk %u seg %llu cnt %llu idxhdr %llu groups %llu chain %llu redraw %llu prevgrp %llu eps %llu\n", \
+               blockIdx.x, (unsigned long long)(k3t[1] - k3t[0]), (unsigned long long)(k3t[2] - k3t[1]),       \
                (unsigned long long)(k3t[3] - k3t[2]), (unsigned long long)(k3t[4] - k3t[3]),                    \
                (unsigned long long)(k3t[5] - k3t[4]), (unsigned long long)(k3t[6] - k3t[5]),                    \
-               (unsigned long long)(k3t[7] - k3t[5]), (unsigned long long)(k3t[8] - k3t[7]),                    \
-               (unsigned long long)(k3t[9] - k3t[8]), (unsigned long long)(k3t[10] - k3t[9]),                   \
-               (unsigned long long)(k3t[6] - k3t[10]))
+               (unsigned long long)(k3t[7] - k3t[6]), (unsigned long long)(k3t[8] - k3t[7]))
 #else
 #define K3T(i)
 #define K3T_DECL
@@ -377,8 +378,16 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 
 // Combine one run r of a slice. Returns false when the run must be recomputed by the retry path.
 // nsw: K3_SCRATCH words of per-run scratch at stride nss (device: the lane's LDS column): the list counts of
-// the run's segments, then the record indices of the episodes that apply.
-constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = 32, K3_SCRATCH = K3_SEG_MAX + K3_EP_MAX;
+// the run's segments (later the first blocks of the candidate episodes), the candidates' record indices, and
+// their (end << 2 | ended << 1 | unusable) words.
+//
+// K3 is latency-bound (one lane per run, a fraction of a wave per SIMD): its time is the number of dependent
+// memory rounds. The reads are ordered so that independent ones share a round and the episode reads stay in
+// flight behind the end-of-run search: (1) segment sums; (2) list counts + per-owner counts; (3) slot
+// indices; (4) episode headers + group sums; (5) the end group's records + the first candidates' deltas,
+// which land while the end group is redrawn. The episode chain is built from the headers without the end
+// block (the episodes are in block order, so the end only truncates it) and cut once the redraw found it.
+constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = 32, K3_SCRATCH = K3_SEG_MAX + 2 * K3_EP_MAX;
 template <int M>
 MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M],
                          uint32_t *nsw, size_t nss)
@@ -392,7 +401,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     }
     // 1. Segment containing the end of the run: the first whose last block is found at >= D. The sums are
     // loaded KB at a time (independent loads in flight together), then scanned.
-    constexpr uint32_t KB = 8;
+    constexpr uint32_t KB = 16;
     int64_t T = 0;
     int e = -1;
     for (uint32_t j0 = 0; j0 < a.nseg && e < 0; j0 += KB) {
@@ -412,8 +421,16 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     }
     K3T(1);
     if (e < (int)a.band_lo) return false;  // past the pre-generated draws or outside the band
-    {  // per-owner counts of the segments before e, KB segments' loads in flight together (no early exit
-       // between them: a fall-through in any of them is checked once at the end)
+    constexpr uint32_t EP_MAX = K3_EP_MAX, SEG_MAX = K3_SEG_MAX;
+    const bool fits = (uint32_t)e < SEG_MAX;
+    // 2. List counts of segments 0..e (issued first) and per-owner counts of the segments before e, in one
+    // round (no early exit between them: a fall-through in any segment is checked once at the end).
+    uint32_t nsv[SEG_MAX];
+    if (fits) {
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_MAX; ++j) nsv[j] = a.nslow[(size_t)(j <= (uint32_t)e ? j : (uint32_t)e) * a.nr + r];
+    }
+    {
         uint32_t ft = 0;
         for (int j0 = 0; j0 < e; j0 += (int)KB) {
             uint32_t c[KB][CNT_WORDS];
@@ -440,10 +457,59 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         }
         if (ft) return false;  // PickFinder fell through (owner 15): the retry kernel reports it
     }
+    uint32_t tot = 0;
+    if (fits) {
+#pragma unroll
+        for (uint32_t j = 0; j < SEG_MAX; ++j) {
+            const uint32_t v = j <= (uint32_t)e ? nsv[j] : 0u;
+            if (v > a.cap) return false;
+            tot += v;
+            nsw[j * nss] = v;  // read back below at data-dependent positions
+        }
+    }
     K3T(2);
-    // 2. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Group sums
+    // 3. The run's episodes in block order (segments 0..e): record indices, then headers. The header loads
+    // are not waited for here: they stay in flight through the group search.
+    const bool batched = fits && tot <= EP_MAX;
+    uint32_t st[EP_MAX], en[EP_MAX], fl[EP_MAX];
+    bool bad_idx = false;
+    if (batched) {
+        uint32_t idx[EP_MAX];
+        {
+            uint32_t j = 0, c = 0, nj = nsw[0];  // (segment, slot) of entry t; nj = count of segment j
+#pragma unroll
+            for (uint32_t t = 0; t < EP_MAX; ++t) {
+                uint32_t v = 0;
+                if (t < tot) {
+                    while (c >= nj) {
+                        ++j;
+                        c = 0;
+                        nj = nsw[j * nss];
+                    }
+                    v = a.slots[((size_t)j * a.cap + c) * a.nr + r];  // issued without waiting for the last
+                    ++c;
+                }
+                idx[t] = v;
+            }
+        }
+#pragma unroll
+        for (uint32_t t = 0; t < EP_MAX; ++t) {
+            st[t] = en[t] = fl[t] = 0;
+            if (t < tot) {
+                bad_idx |= idx[t] >= a.lcap;
+                const uint32_t i = idx[t] < a.lcap ? idx[t] : 0u;
+                const uint32_t *rec = a.recs + (size_t)i * a.rec_words;
+                st[t] = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
+                en[t] = rec[0];
+                fl[t] = rec[1];
+                nsw[(SEG_MAX + t) * nss] = idx[t];
+            }
+        }
+    }
+    K3T(3);
+    // 4. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Group sums
     // KG at a time, as above (a segment has up to a few hundred groups).
-    constexpr uint32_t KG = 32;
+    constexpr uint32_t KG = 72;
     const size_t gb = (size_t)(e - (int)a.band_lo) * a.gps;
     uint32_t G = a.gps;
     for (uint32_t g0 = 0; g0 < a.gps && G == a.gps; g0 += KG) {
@@ -458,15 +524,56 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             }
         }
     }
-    if (G == a.gps) return false;
-    K3T(3);
-    if (add_packed<M>(F, a.gcum + (gb + G) * CNT_WORDS * a.nr + r, a.nr)) return false;
+    if (G == a.gps || bad_idx) return false;
+    K3T(4);
+    // 5. The end group's stream record and counters are issued, then the candidate chain is built from the
+    // headers (an episode is a candidate when its first block is reached quiet, ignoring the end of the run),
+    // then the first APPLY_B candidates' deltas are issued; the group redraw waits for the stream record only.
+    const GroupRec gr = a.grec[(gb + G) * a.nr + r];
+    uint32_t gc[CNT_WORDS];
+#pragma unroll
+    for (uint32_t w = 0; w < CNT_WORDS; ++w)
+        gc[w] = (w < (uint32_t)(M + 1) / 2 || w == CNT_WORDS - 1) ? a.gcum[((gb + G) * CNT_WORDS + w) * a.nr + r] : 0u;
+    constexpr uint32_t APPLY_B = 8;
+    uint32_t na = 0;
+    uint32_t d[APPLY_B][2 * M];
+    if (batched) {
+        uint32_t cursor = 0;
+        bool stop = false;
+#pragma unroll
+        for (uint32_t t = 0; t < EP_MAX; ++t) {
+            if (stop || t >= tot || st[t] < cursor) continue;  // consumed by the previous candidate
+            const bool ended = (fl[t] & REC_ENDED) != 0u;
+            nsw[na * nss] = st[t];
+            nsw[(SEG_MAX + na) * nss] = nsw[(SEG_MAX + t) * nss];  // na <= t: compacts in place
+            nsw[(SEG_MAX + EP_MAX + na) * nss] =
+                (en[t] << 2) | (ended ? 2u : 0u) | ((fl[t] & (REC_ERR | REC_SKIP)) ? 1u : 0u);
+            ++na;
+            cursor = en[t];
+            stop = ended;  // the run ended inside this episode
+        }
+        if (na) {
+#pragma unroll
+            for (uint32_t b = 0; b < APPLY_B; ++b) {
+                const uint32_t t = b < na ? b : na - 1;  // clamped: unconditional loads, masked below
+                const uint32_t *rec = a.recs + (size_t)nsw[(SEG_MAX + t) * nss] * a.rec_words;
+#pragma unroll
+                for (int k = 0; k < 2 * M; ++k) d[b][k] = rec[2 + k];
+            }
+        }
+    }
+    K3T(5);
+#pragma unroll
+    for (int w = 0; w < (M + 1) / 2; ++w) {
+        F[2 * w] += gc[w] & 0xFFFFu;
+        if (2 * w + 1 < M) F[2 * w + 1] += gc[w] >> 16;
+    }
+    if (gc[CNT_WORDS - 1] >> 16) return false;
     const uint32_t bg = (uint32_t)e * a.seg + G * GROUP;
     uint32_t n_end = 0, klast = 15u;
     int64_t t_last = 0;
     bool done = false;
     {  // redraw the group from its first block's stored streams
-        const GroupRec gr = a.grec[(gb + G) * a.nr + r];
         Rng ri = gr.ri, rp = gr.rp;
         uint32_t wd = gr.w0;
         for (uint32_t q = 0; q < GROUP; ++q) {
@@ -486,117 +593,54 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         }
     }
     if (!done) return false;
-    K3T(4);
+    K3T(6);
     if (n_end == bg && n_end > 0) {  // the block before the end is the previous group's last one
         size_t pg;
         if (G > 0) pg = gb + G - 1;
         else if (e > (int)a.band_lo) pg = gb - 1;
         else return false;
-        const GroupRec gr = a.grec[pg * a.nr + r];
-        Rng ri = gr.ri, rp = gr.rp;
-        uint32_t wd = gr.w0;
+        const GroupRec gp = a.grec[pg * a.nr + r];
+        Rng ri = gp.ri, rp = gp.rp;
+        uint32_t wd = gp.w0;
         for (uint32_t q = 1; q < GROUP; ++q) wd = draw_word(ri, rp, a.tab.logt, a.tab.pick);
         klast = wd & 15u;
     }
-    // 3. Episodes in block order; an episode applies when its first block is reached quiet. The reads are
-    // gathered in three batches (list counts of segments 0..e, their slot indices, the records' headers), so
-    // a run waits for three rounds of memory latency instead of one per segment and two per episode; a run
-    // with more than EP_MAX episodes up to its end segment (never at BASELINE sizes: ~rho * blocks, 9 for
-    // configs[1]) takes the same walk one read at a time.
-    K3T(5);
-    uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
-    constexpr uint32_t EP_MAX = K3_EP_MAX, SEG_MAX = K3_SEG_MAX;
-    uint32_t tot = 0;
-    const bool fits = (uint32_t)e < SEG_MAX;
-    if (fits) {
-        uint32_t nsv[SEG_MAX];
-#pragma unroll
-        for (uint32_t j = 0; j < SEG_MAX; ++j) {
-            const uint32_t v = a.nslow[(size_t)(j <= (uint32_t)e ? j : (uint32_t)e) * a.nr + r];
-            nsv[j] = j <= (uint32_t)e ? v : 0u;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < SEG_MAX; ++j) {
-            if (nsv[j] > a.cap) return false;
-            tot += nsv[j];
-            nsw[j * nss] = nsv[j];  // read back below at data-dependent positions
-        }
-    }
     K3T(7);
-    if (fits && tot <= EP_MAX) {
-        uint32_t idx[EP_MAX];
-        {
-            uint32_t j = 0, c = 0, nj = nsw[0];  // (segment, slot) of entry t; nj = count of segment j
-#pragma unroll
-            for (uint32_t t = 0; t < EP_MAX; ++t) {
-                uint32_t v = 0;
-                if (t < tot) {
-                    while (c >= nj) {
-                        ++j;
-                        c = 0;
-                        nj = nsw[j * nss];
-                    }
-                    v = a.slots[((size_t)j * a.cap + c) * a.nr + r];  // issued without waiting for the last
-                    ++c;
-                }
-                idx[t] = v;
-            }
+    // 6. Episodes: the candidates that start before the end apply (a prefix of the chain).
+    uint32_t cursor = 0;  // first block not consumed yet; ~0 once the run ended inside an episode
+    if (batched) {
+        uint32_t naf = 0;
+        for (uint32_t t = 0; t < na && nsw[t * nss] < n_end; ++t) {
+            const uint32_t x = nsw[(SEG_MAX + EP_MAX + t) * nss];
+            if (x & 1u) return false;  // an applied episode K2 could not finish, or one it skipped
+            cursor = (x & 2u) ? 0xFFFFFFFFu : (x >> 2);
+            ++naf;
         }
-        K3T(8);
-        uint32_t st[EP_MAX], en[EP_MAX], fl[EP_MAX];
 #pragma unroll
-        for (uint32_t t = 0; t < EP_MAX; ++t) {
-            st[t] = en[t] = fl[t] = 0;
-            if (t < tot) {
-                if (idx[t] >= a.lcap) return false;
-                const uint32_t *rec = a.recs + (size_t)idx[t] * a.rec_words;
-                st[t] = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
-                en[t] = rec[0];
-                fl[t] = rec[1];
-            }
-        }
-        K3T(9);
-        // which episodes apply: the chain over the headers alone (registers); their record indices go to the
-        // lane's scratch column so that the deltas are then loaded APPLY_B episodes at a time
-        bool stop = false;
-        uint32_t na = 0;
+        for (uint32_t b = 0; b < APPLY_B; ++b)
 #pragma unroll
-        for (uint32_t t = 0; t < EP_MAX; ++t) {
-            if (stop || t >= tot) continue;
-            if (st[t] >= n_end) {  // no later episode starts before the end of the run
-                stop = true;
-                continue;
+            for (int k = 0; k < M; ++k) {
+                F[k] += b < naf ? d[b][k] : 0u;
+                S[k] += b < naf ? d[b][M + k] : 0u;
             }
-            if (st[t] < cursor) continue;  // consumed by the previous episode
-            if (fl[t] & (REC_ERR | REC_SKIP)) return false;
-            nsw[(SEG_MAX + na) * nss] = idx[t];
-            ++na;
-            cursor = en[t];
-            if (fl[t] & REC_ENDED) {  // the run ended inside this episode
-                cursor = 0xFFFFFFFFu;
-                stop = true;
-            }
-        }
-        K3T(10);
-        constexpr uint32_t APPLY_B = 4;
-        for (uint32_t t0 = 0; t0 < na; t0 += APPLY_B) {
-            uint32_t d[APPLY_B][2 * M];
+        for (uint32_t t0 = APPLY_B; t0 < naf; t0 += APPLY_B) {  // more than APPLY_B applied episodes (rare)
+            uint32_t dd[APPLY_B][2 * M];
 #pragma unroll
             for (uint32_t b = 0; b < APPLY_B; ++b) {
-                const uint32_t t = t0 + b < na ? t0 + b : na - 1;  // clamped: unconditional loads, masked below
+                const uint32_t t = t0 + b < naf ? t0 + b : naf - 1;
                 const uint32_t *rec = a.recs + (size_t)nsw[(SEG_MAX + t) * nss] * a.rec_words;
 #pragma unroll
-                for (int k = 0; k < 2 * M; ++k) d[b][k] = rec[2 + k];
+                for (int k = 0; k < 2 * M; ++k) dd[b][k] = rec[2 + k];
             }
 #pragma unroll
             for (uint32_t b = 0; b < APPLY_B; ++b)
 #pragma unroll
                 for (int k = 0; k < M; ++k) {
-                    F[k] += t0 + b < na ? d[b][k] : 0u;
-                    S[k] += t0 + b < na ? d[b][M + k] : 0u;
+                    F[k] += t0 + b < naf ? dd[b][k] : 0u;
+                    S[k] += t0 + b < naf ? dd[b][M + k] : 0u;
                 }
         }
-    } else {
+    } else {  // more than EP_MAX episodes up to the end segment (never at BASELINE sizes): one read at a time
         bool stop = false;
         for (int j = 0; j <= e && !stop; ++j) {
             const uint32_t ns = a.nslow[(size_t)j * a.nr + r];
@@ -627,9 +671,9 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
             }
         }
     }
-    K3T(6);
+    K3T(8);
     K3T_PRINT;
-    // 4. The run ended quiet and its last block was a fast one: it counts only if it arrived by D.
+    // 7. The run ended quiet and its last block was a fast one: it counts only if it arrived by D.
     if (cursor != 0xFFFFFFFFu && n_end > 0 && cursor < n_end) {
         const uint32_t k = klast;
         int64_t pk = 0;
@@ -676,8 +720,8 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     src.nxt = e.w1;
     src.have_nxt = true;
     // K2's capacities: MSIM_K2_NX extra in-flight blocks (an episode that needs more flags its run, which
-    // the retry kernel recomputes with NX_WIDE), deep branches on
-    Sim<M, false, true, MSIM_K2_NX, NG_FAST> s;
+    // the retry kernel recomputes with NX_WIDE), deep branches per MSIM_K2_DEEP
+    Sim<M, false, (bool)MSIM_K2_DEEP, MSIM_K2_NX, NG_FAST> s;
     EpisodeOut<M> o;
     s.episode(p, src, T, o);
     rec[0] = o.end;

@@ -5,7 +5,7 @@
 # count whose object is replaced (default 9).
 set -e
 cd "$(dirname "$0")/../miningsimulation_amd/csrc"
-make -s
+make -s -j8
 SRC=$2
 BASE=${SRC%.hip}
 M=${4:-9}

@@ -18,6 +18,16 @@ def _ensure(path: str, builder) -> None:
         builder()
 
 
+def _stale(outs) -> bool:
+    """True when a header or source the host builds compile is newer than one of their outputs."""
+    srcs = []
+    for d, exts in ((os.path.join(ROOT, "miningsimulation_amd", "csrc"), (".h",)),
+                    (os.path.join(ROOT, "tests", "native"), (".cpp", ".h"))):
+        srcs += [os.path.join(d, f) for f in os.listdir(d) if f.endswith(exts)]
+    newest = max(os.path.getmtime(f) for f in srcs)
+    return min(os.path.getmtime(p) for p in outs) < newest
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import pyoracle
@@ -37,7 +47,8 @@ def native_tests():
     wide = os.path.join(ROOT, "build", "libwide_host.so")
     sel = os.path.join(ROOT, "build", "libsel_host.so")
     gen = os.path.join(ROOT, "build", "libgeneral_host.so")
-    if not all(os.path.exists(p) for p in (lib, chk, pipe, wide, sel, gen)):
+    outs = (lib, chk, pipe, wide, sel, gen)
+    if not all(os.path.exists(p) for p in outs) or _stale(outs):
         ge.build_native_tests()
     return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel,
             "general_host": gen}
