@@ -129,7 +129,14 @@ struct DevCtx {
 #pragma unroll
         for (uint32_t w = 0; w < CNT_WORDS; ++w) a.gcum[(gi * CNT_WORDS + w) * a.nr + r] = packed(w);
     }
-    __device__ void group(uint32_t g, uint32_t sum) { a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum; }
+    __device__ void group(uint32_t g, uint32_t sum, uint64_t end)
+    {
+        a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum;
+        if (g % SGROUP == SGROUP - 1 || g + 1 == a.gps) {
+            const uint32_t nsg = (a.gps + SGROUP - 1) / SGROUP;
+            a.gend[((size_t)jb * nsg + g / SGROUP) * a.nr + run()] = end;
+        }
+    }
 };
 
 // Resident K1 waves per SIMD the register budget is sized for (VGPRs <= 512 / waves). Measured on MI355X

@@ -158,23 +158,22 @@ __global__ __launch_bounds__(TPB, 2) void msim_sweep_kernel(const SimParams *__r
 __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
 
 // K2: one lane per listed non-fast block (msim_pipeline.h episode_entry).
-// Three resident waves per SIMD (168 VGPRs, some spills at the episode's entry) rather than the two that 207
-// spill-free VGPRs allow: measured on MI355X (profiles/r03/k3ab), c2 with two overlapping streams 9.15M ->
-// 9.37M run-years/s, serial unchanged (K2 shares the GPU with the next step's K1 better).
+// Three resident waves per SIMD (168 VGPRs): the lean state machine fits them without spills; four waves
+// (128 VGPRs) spill and run slower (136.6 vs 79.6 us, profiles/r04/k2v2).
 #ifndef MSIM_K2_WAVES
 #define MSIM_K2_WAVES 3
 #endif
 // Workgroup sizes of K2 and K3. K3 has one lane per run, so a 256-lane workgroup put the 32 768 runs of a c2
 // slice on 128 workgroups, half the CUs; one-wave workgroups spread them over all 256.
 #ifndef MSIM_K2_TPB
-#define MSIM_K2_TPB 256
+#define MSIM_K2_TPB 64  // one-wave workgroups: a finished wave's slot takes new work at once (K2 79.6 -> 76.7 us)
 #endif
 #ifndef MSIM_K3_TPB
 #define MSIM_K3_TPB 64
 #endif
 constexpr int K2_TPB = MSIM_K2_TPB, K3_TPB = MSIM_K3_TPB;
 static_assert(K3_TPB % 64 == 0 && K3_TPB <= TPB && TPB % K3_TPB == 0, "K3 workgroups: whole waves, dividing TPB");
-template <int M>
+template <int M, bool LEAN>
 __global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_WAVES, 8))) void msim_episode_kernel(const SimParams p,
                                                                                                     const PipeArgs a)
 {
@@ -190,7 +189,7 @@ __global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_
     la.tab.pick = &s_pick;
     const uint32_t cnt = *a.list_count;
     const uint32_t lim = cnt < a.lcap ? cnt : a.lcap;
-    for (uint32_t idx = blockIdx.x * K2_TPB + threadIdx.x; idx < lim; idx += gridDim.x * K2_TPB) episode_entry<M>(p, la, idx);
+    for (uint32_t idx = blockIdx.x * K2_TPB + threadIdx.x; idx < lim; idx += gridDim.x * K2_TPB) episode_entry<M, LEAN>(p, la, idx);
 }
 
 // K3: one lane per run (msim_pipeline.h combine_run), then the MinerStats reduction.
@@ -286,6 +285,7 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     pa.nslow = (const uint32_t *)(ws + L.nslow_off);
     pa.slots = (const uint32_t *)(ws + L.slots_off);
     pa.gsum = (const uint32_t *)(ws + L.gsum_off);
+    pa.gend = (const uint64_t *)(ws + L.gend_off);
     pa.gcum = (const uint32_t *)(ws + L.gcum_off);
     pa.grec = (const GroupRec *)(ws + L.grec_off);
     pa.list = (const EpEntry *)(ws + L.list_off);
@@ -306,6 +306,7 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.nslow = (uint32_t *)(ws + L.nslow_off);
     da.slots = (uint32_t *)(ws + L.slots_off);
     da.gsum = (uint32_t *)(ws + L.gsum_off);
+    da.gend = (uint64_t *)(ws + L.gend_off);
     da.gcum = (uint32_t *)(ws + L.gcum_off);
     da.grec = (GroupRec *)(ws + L.grec_off);
     da.list = (EpEntry *)(ws + L.list_off);
@@ -327,7 +328,8 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
         hipError_t e = launch_draws(da, a.stream);
         if (ee) (void)hipEventRecord(ee, a.stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((msim_episode_kernel<M>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
+        if (L.k2_lean) hipLaunchKernelGGL((msim_episode_kernel<M, true>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
+        else hipLaunchKernelGGL((msim_episode_kernel<M, false>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
         hipLaunchKernelGGL((msim_combine_kernel<M>), dim3((cn + K3_TPB - 1) / K3_TPB), dim3(K3_TPB), 0, a.stream, a.p, pa,
                            cn, off, parts + (size_t)(off / K3_TPB) * 6 * M, a.records, a.best_h, a.err_count, a.err_list,
                            a.err_cap);

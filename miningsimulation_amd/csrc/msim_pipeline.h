@@ -30,13 +30,15 @@
 
 namespace msim {
 
-#ifndef MSIM_K2_NX
-#define MSIM_K2_NX NX_FAST  // K2's extra in-flight blocks (measured: NX_WIDE 150 us vs NX_FAST 141 us per c2 launch)
-#endif
-#ifndef MSIM_K2_DEEP
-#define MSIM_K2_DEEP 1  // K2 follows forks deeper than the 16-height window (else such episodes flag their run)
-#endif
+// K2's state machine comes in two sizes. The lean one (networks with rho <= K2_LEAN_RHO) holds 2 extra
+// in-flight blocks and no deep-branch counters: an episode that needs more (a miner with 4 of its own blocks in
+// flight, or a fork deeper than the 16-height window) flags its run, which the retry kernel recomputes. At
+// rho <= 0.002 that is < 1e-3 of the runs of a 12-month simulation; configs[1] (rho = 1.7e-4): K2 125 -> 77 us
+// per launch (no spills instead of 134 VGPR spills; profiles/r04/k2v). Above it the full capacities (4 extra
+// blocks, deep branches) keep the retries rare.
+constexpr double K2_LEAN_RHO = 0.002;
 constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
+constexpr uint32_t SGROUP = 8;          // groups per super-group (K3 searches super-group ends, then groups)
 constexpr uint32_t MIN_SEG = 512;       // shortest K1 worker (keeps the jump-ahead cost < 5 %)
 constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pairs (<= 16 owners)
 #ifndef MSIM_K1_QB
@@ -64,6 +66,7 @@ struct PipeLayout {
     uint32_t nr;       // runs in a slice (multiple of 256)
     uint32_t seg;      // blocks per K1 worker (multiple of GROUP)
     uint32_t gps;      // groups per segment (seg / GROUP)
+    uint32_t nsg;      // super-groups per segment (ceil(gps / SGROUP))
     uint32_t nseg;     // segments (K1 workers) per run
     uint32_t nb;       // nseg * seg pre-generated blocks per run
     uint32_t cap;      // slow-block slots per (run, segment)
@@ -71,7 +74,8 @@ struct PipeLayout {
     uint32_t nband;
     uint32_t lcap;     // episode list capacity
     uint32_t rec_words;
-    size_t segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gcum_off, grec_off, list_off, recs_off,
+    uint32_t k2_lean;  // K2 runs the lean state machine (rho <= K2_LEAN_RHO)
+    size_t segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gend_off, gcum_off, grec_off, list_off, recs_off,
         count_off, total;
 };
 
@@ -93,6 +97,7 @@ struct DrawArgs {
     uint32_t *nslow;      // [nseg][nr]
     uint32_t *slots;      // [nseg][cap][nr]
     uint32_t *gsum;       // [nband][gps][nr]
+    uint64_t *gend;       // [nband][nsg][nr]: time from the segment's start to the end of each super-group
     uint32_t *gcum;       // [nband][gps][8][nr]
     GroupRec *grec;       // [nband][gps][nr]
     EpEntry *list;        // [lcap]
@@ -107,6 +112,7 @@ struct PipeArgs {  // K2 / K3
     const uint32_t *nslow;
     const uint32_t *slots;
     const uint32_t *gsum;
+    const uint64_t *gend;
     const uint32_t *gcum;
     const GroupRec *grec;
     const EpEntry *list;
@@ -133,9 +139,10 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     const uint64_t want = (n_runs + 255) / 256 * 256;
     // slice size first (memory), with an upper estimate of the per-run bytes
     L.rec_words = 3 + 2 * m;
+    L.k2_lean = rho <= K2_LEAN_RHO ? 1u : 0u;
     const double nb_est = need + 2.0 * MIN_SEG;
     const double per_run = 64.0 * (8.0 + CNT_WORDS * 4 + 4) + 4.0 * (rho * nb_est * 2 + 64.0 * 16) +
-                           2.0 * nb_est / GROUP * (4.0 + CNT_WORDS * 4 + sizeof(GroupRec)) +
+                           2.0 * nb_est / GROUP * (4.0 + 8.0 / SGROUP + CNT_WORDS * 4 + sizeof(GroupRec)) +
                            rho * nb_est * (sizeof(EpEntry) + 4.0 * L.rec_words);
     uint64_t cap_runs = (uint64_t)(budget / per_run) / 256 * 256;
     if (cap_runs < 256) cap_runs = 256;
@@ -159,6 +166,7 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     L.seg = (uint32_t)ceil(need / best_w / GROUP) * GROUP;
     if (L.seg < GROUP) L.seg = GROUP;
     L.gps = L.seg / GROUP;
+    L.nsg = (L.gps + SGROUP - 1) / SGROUP;
     L.nb = L.nseg * L.seg;
     const double lo = mu - 8.0 * sd - 64.0;
     L.band_lo = lo > 0 ? (uint32_t)floor(lo / L.seg) : 0u;
@@ -179,6 +187,8 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     o = al(o + (size_t)L.nseg * L.cap * L.nr * 4);
     L.gsum_off = o;
     o = al(o + (size_t)L.nband * L.gps * L.nr * 4);
+    L.gend_off = o;
+    o = al(o + (size_t)L.nband * L.nsg * L.nr * 8);
     L.gcum_off = o;
     o = al(o + (size_t)L.nband * L.gps * CNT_WORDS * L.nr * 4);
     L.grec_off = o;
@@ -275,7 +285,8 @@ MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, cons
 //                                     called after a nonzero vote: records a non-fast block when s
 //                                     (offset = its find time minus the segment's start; its word, the
 //                                     next one and both streams after them)
-//   group(g, sum)                     band only: sum of the group's intervals
+//   group(g, sum, end)                band only: sum of the group's intervals, and the time from the segment's
+//                                     start to the group's end
 //   quad()                            start of a quad of blocks
 //   group_start(g, w0, ri, rp)        band only: before group g's first block (its word and the streams
 //                                     after it; snapshot the counters)
@@ -338,7 +349,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
                 infocur = info[q];
             }
         }
-        if (band) cx.group(g, gacc);
+        if (band) cx.group(g, gacc, tsum + gacc);
         tsum += gacc;
     }
     return tsum;
@@ -384,7 +395,8 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 // K3 is latency-bound (one lane per run, a fraction of a wave per SIMD): its time is the number of dependent
 // memory rounds. The reads are ordered so that independent ones share a round and the episode reads stay in
 // flight behind the end-of-run search: (1) segment sums; (2) list counts + per-owner counts; (3) slot
-// indices; (4) episode headers + group sums; (5) the end group's records + the first candidates' deltas,
+// indices; (4) episode headers + super-group ends; (5) group sums; (6) the end group's records + the first
+// candidates' deltas,
 // which land while the end group is redrawn. The episode chain is built from the headers without the end
 // block (the episodes are in block order, so the end only truncates it) and cut once the redraw found it.
 constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = 32, K3_SCRATCH = K3_SEG_MAX + 2 * K3_EP_MAX;
@@ -507,17 +519,37 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         }
     }
     K3T(3);
-    // 4. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Group sums
-    // KG at a time, as above (a segment has up to a few hundred groups).
-    constexpr uint32_t KG = 72;
+    // 4. Group, then block, where T first reaches D: n_end = #{i : T_i < D} (main.cpp:150,153). Two rounds: the
+    // ends of the segment's super-groups (time from the segment's start, KS at a time), then the SGROUP group
+    // sums of the super-group that reaches D.
     const size_t gb = (size_t)(e - (int)a.band_lo) * a.gps;
+    const uint32_t nsg = (a.gps + SGROUP - 1) / SGROUP;
+    const size_t sb = (size_t)(e - (int)a.band_lo) * nsg;
+    constexpr uint32_t KS = 24;
+    uint32_t sg = nsg;
+    uint64_t base = 0;  // time from the segment's start to the start of super-group sg
+    for (uint32_t s0 = 0; s0 < nsg && sg == nsg; s0 += KS) {
+        uint64_t ps[KS];
+#pragma unroll
+        for (uint32_t j = 0; j < KS; ++j) ps[j] = a.gend[(sb + (s0 + j < nsg ? s0 + j : nsg - 1)) * a.nr + r];
+#pragma unroll
+        for (uint32_t j = 0; j < KS; ++j) {
+            if (sg == nsg && s0 + j < nsg) {
+                if (T + (int64_t)ps[j] >= D) sg = s0 + j;
+                else base = ps[j];
+            }
+        }
+    }
+    if (sg == nsg) return false;
+    T += (int64_t)base;
     uint32_t G = a.gps;
-    for (uint32_t g0 = 0; g0 < a.gps && G == a.gps; g0 += KG) {
-        uint32_t gs[KG];
+    {
+        const uint32_t g0 = sg * SGROUP;
+        uint32_t gs[SGROUP];
 #pragma unroll
-        for (uint32_t g = 0; g < KG; ++g) gs[g] = a.gsum[(gb + (g0 + g < a.gps ? g0 + g : a.gps - 1)) * a.nr + r];
+        for (uint32_t g = 0; g < SGROUP; ++g) gs[g] = a.gsum[(gb + (g0 + g < a.gps ? g0 + g : a.gps - 1)) * a.nr + r];
 #pragma unroll
-        for (uint32_t g = 0; g < KG; ++g) {
+        for (uint32_t g = 0; g < SGROUP; ++g) {
             if (G == a.gps && g0 + g < a.gps) {
                 if (T + (int64_t)gs[g] >= D) G = g0 + g;
                 else T += (int64_t)gs[g];
@@ -573,23 +605,34 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     uint32_t n_end = 0, klast = 15u;
     int64_t t_last = 0;
     bool done = false;
-    {  // redraw the group from its first block's stored streams
+    {  // redraw the group from its first block's stored streams, four blocks at a time as K1 drew them
+       // (draw_quad_fast, the exact form for a flagged quad): the four draws' table reads and interval
+       // polynomials are independent, so they overlap instead of forming one chain of 31 draws
         Rng ri = gr.ri, rp = gr.rp;
-        uint32_t wd = gr.w0;
-        for (uint32_t q = 0; q < GROUP; ++q) {
-            if (q) wd = draw_word(ri, rp, a.tab.logt, a.tab.pick);
-            const int64_t Tn = T + (int64_t)(wd >> 5);
-            if (Tn >= D) {
-                done = true;
-                n_end = bg + q;
-                t_last = T;
-                break;
-            }
-            T = Tn;
-            klast = wd & 15u;
-            if (klast == 15u) return false;  // PickFinder fell through (simulation.h:220): the retry reports it
+        uint32_t Ic = gr.w0 >> 5, kc = gr.w0 & 15u;  // the current block (q) and its finder
+        for (uint32_t q0 = 0; q0 < GROUP && !done; q0 += K1_QB) {
+            uint32_t I[K1_QB], info[K1_QB];
+            const Rng ri0 = ri, rp0 = rp;
+            if (draw_quad_fast(ri, rp, a.tab.logt, a.tab.pick, MSIM_FD_DEFAULT, I, info))
+                draw_quad_exact(ri0, rp0, a.tab.logt, a.tab.pick, I, info);
 #pragma unroll
-            for (int kk = 0; kk < M; ++kk) F[kk] += (klast == (uint32_t)kk) ? 1u : 0u;
+            for (uint32_t b = 0; b < K1_QB; ++b) {
+                if (done) continue;
+                const int64_t Tn = T + (int64_t)Ic;
+                if (Tn >= D) {
+                    done = true;
+                    n_end = bg + q0 + b;
+                    t_last = T;
+                    continue;
+                }
+                T = Tn;
+                klast = kc;
+                if (klast == 15u) return false;  // PickFinder fell through (simulation.h:220): the retry reports it
+#pragma unroll
+                for (int kk = 0; kk < M; ++kk) F[kk] += (klast == (uint32_t)kk) ? 1u : 0u;
+                Ic = I[b];
+                kc = info_finder(info[b]);
+            }
         }
     }
     if (!done) return false;
@@ -600,10 +643,10 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
         else if (e > (int)a.band_lo) pg = gb - 1;
         else return false;
         const GroupRec gp = a.grec[pg * a.nr + r];
-        Rng ri = gp.ri, rp = gp.rp;
-        uint32_t wd = gp.w0;
-        for (uint32_t q = 1; q < GROUP; ++q) wd = draw_word(ri, rp, a.tab.logt, a.tab.pick);
-        klast = wd & 15u;
+        // only the finder of its last block is needed: the picker stream alone, stepped to block GROUP - 1
+        Rng rp = gp.rp;
+        for (uint32_t q = 1; q + 1 < GROUP; ++q) rng_next(rp);
+        klast = info_finder(pick_info(rng_next(rp), a.tab.pick));
     }
     K3T(7);
     // 6. Episodes: the candidates that start before the end apply (a prefix of the chain).
@@ -689,7 +732,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
 }
 
 // ---------------------------------------------------------------- K2 lane body (shared host/device)
-template <int M>
+template <int M, bool LEAN>
 MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
 {
     const EpEntry e = a.list[idx];
@@ -719,9 +762,8 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     src.cur = e.w0;
     src.nxt = e.w1;
     src.have_nxt = true;
-    // K2's capacities: MSIM_K2_NX extra in-flight blocks (an episode that needs more flags its run, which
-    // the retry kernel recomputes with NX_WIDE), deep branches per MSIM_K2_DEEP
-    Sim<M, false, (bool)MSIM_K2_DEEP, MSIM_K2_NX, NG_FAST> s;
+    // K2's capacities (K2_LEAN_RHO above); the retry kernel recomputes a flagged run with NX_WIDE and deep branches
+    Sim<M, false, !LEAN, LEAN ? 2 : NX_FAST, NG_FAST> s;
     EpisodeOut<M> o;
     s.episode(p, src, T, o);
     rec[0] = o.end;

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-tails}; mkdir -p $O
 if [ -f miningsimulation_amd/variants/libmsim_k3prof.so ]; then
   MSIM_LIB=$PWD/miningsimulation_amd/variants/libmsim_k3prof.so timeout -k 10 120 python -u bench.py --config c2 --steps 1 --warmup 0 --streams 1 --no-cpu-baseline > $O/k3.json 2> $O/k3.err || { tail -20 $O/k3.err; exit 1; }
-  grep K3PROF $O/k3.err | head -12
+  grep -a K3PROF $O/k3.json | head -12
 fi
 for v in default $VARIANTS; do
   if [ $v = default ]; then unset MSIM_LIB; else export MSIM_LIB=$PWD/miningsimulation_amd/variants/libmsim_$v.so; fi

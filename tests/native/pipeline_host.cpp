@@ -21,6 +21,7 @@ struct HostCtx {
     uint32_t r, seg, jb, nsl = 0;
     uint32_t cnt[CNT_WORDS] = {0};
     std::vector<uint32_t> *slots, *gsum, *gcum;
+    std::vector<uint64_t> *gend;
     std::vector<GroupRec> *grec;
     std::vector<EpEntry> *list;
     void count(uint32_t info)
@@ -43,7 +44,11 @@ struct HostCtx {
         (*grec)[((size_t)jb * L.gps + g) * L.nr + r] = GroupRec{ri, rp, w0, 0};
         for (uint32_t w = 0; w < CNT_WORDS; ++w) (*gcum)[(((size_t)jb * L.gps + g) * CNT_WORDS + w) * L.nr + r] = cnt[w];
     }
-    void group(uint32_t g, uint32_t sum) { (*gsum)[((size_t)jb * L.gps + g) * L.nr + r] = sum; }
+    void group(uint32_t g, uint32_t sum, uint64_t end)
+    {
+        (*gsum)[((size_t)jb * L.gps + g) * L.nr + r] = sum;
+        if (g % SGROUP == SGROUP - 1 || g + 1 == L.gps) (*gend)[((size_t)jb * L.nsg + g / SGROUP) * L.nr + r] = end;
+    }
 };
 
 template <int M>
@@ -65,7 +70,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     std::vector<uint32_t> segcnt((size_t)L.nseg * CNT_WORDS * n), nslow((size_t)L.nseg * n),
         slots((size_t)L.nseg * L.cap * n, 0xFFFFFFFFu), gsum((size_t)L.nband * L.gps * n),
         gcum((size_t)L.nband * L.gps * CNT_WORDS * n);
-    std::vector<uint64_t> segsum((size_t)L.nseg * n);
+    std::vector<uint64_t> segsum((size_t)L.nseg * n), gend((size_t)L.nband * L.nsg * n);
     std::vector<EpEntry> list;
     for (uint32_t r = 0; r < n; ++r) {
         const uint64_t run = run_begin + r;
@@ -94,6 +99,7 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
             cx.grec = &grec;
             cx.slots = &slots;
             cx.gsum = &gsum;
+            cx.gend = &gend;
             cx.gcum = &gcum;
             cx.list = &list;
             segsum[(size_t)j * n + r] = draw_segment(cx, ri, rp, &logt, &pick, j * L.seg, L.seg, j >= L.band_lo);
@@ -120,11 +126,15 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     a.nslow = nslow.data();
     a.slots = slots.data();
     a.gsum = gsum.data();
+    a.gend = gend.data();
     a.gcum = gcum.data();
     a.list = list.data();
     a.list_count = &count;
     a.recs = recs.data();
-    for (uint32_t i = 0; i < count; ++i) episode_entry<M>(p, a, i);
+    for (uint32_t i = 0; i < count; ++i) {
+        if (L.k2_lean) episode_entry<M, true>(p, a, i);
+        else episode_entry<M, false>(p, a, i);
+    }
     for (uint32_t r = 0; r < n; ++r) {
         uint32_t F[M], S[M];
         uint32_t nsw[K3_SCRATCH];
