@@ -486,7 +486,10 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
     uint32_t st[EP_MAX], en[EP_MAX], fl[EP_MAX];
     bool bad_idx = false;
     if (batched) {
-        uint32_t idx[EP_MAX];
+        // entry t -> (segment, slot): a walk over the counts in LDS, no memory reads; then every slot index and
+        // every header is loaded without a branch (entries past tot read slot 0 / record 0 and are masked), so
+        // no load waits behind a divergent block for the ones issued before it
+        uint32_t pos[EP_MAX];
         {
             uint32_t j = 0, c = 0, nj = nsw[0];  // (segment, slot) of entry t; nj = count of segment j
 #pragma unroll
@@ -498,24 +501,25 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
                         c = 0;
                         nj = nsw[j * nss];
                     }
-                    v = a.slots[((size_t)j * a.cap + c) * a.nr + r];  // issued without waiting for the last
+                    v = j * a.cap + c;
                     ++c;
                 }
-                idx[t] = v;
+                pos[t] = v;
             }
         }
+        uint32_t idx[EP_MAX];
+#pragma unroll
+        for (uint32_t t = 0; t < EP_MAX; ++t) idx[t] = a.slots[(size_t)pos[t] * a.nr + r];
 #pragma unroll
         for (uint32_t t = 0; t < EP_MAX; ++t) {
-            st[t] = en[t] = fl[t] = 0;
-            if (t < tot) {
-                bad_idx |= idx[t] >= a.lcap;
-                const uint32_t i = idx[t] < a.lcap ? idx[t] : 0u;
-                const uint32_t *rec = a.recs + (size_t)i * a.rec_words;
-                st[t] = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
-                en[t] = rec[0];
-                fl[t] = rec[1];
-                nsw[(SEG_MAX + t) * nss] = idx[t];
-            }
+            const bool in = t < tot;
+            bad_idx |= in && idx[t] >= a.lcap;
+            const uint32_t i = in && idx[t] < a.lcap ? idx[t] : 0u;
+            const uint32_t *rec = a.recs + (size_t)i * a.rec_words;
+            st[t] = rec[2 + 2 * M];  // the episode's first block (K2 copies it from the list entry)
+            en[t] = rec[0];
+            fl[t] = rec[1];
+            nsw[(SEG_MAX + t) * nss] = i;
         }
     }
     K3T(3);
