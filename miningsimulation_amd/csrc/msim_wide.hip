@@ -311,6 +311,21 @@ __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a
 }
 
 // ---------------------------------------------------------------- W3
+// Phase timing (diagnostic builds only, -DW3_PROF=1: scripts/build_variant.sh): clocks at each phase of a run
+// for the first wave of a few workgroups, summed over the runs the wave combines.
+#if defined(W3_PROF) && W3_PROF
+#define W3T(i) w3c[i] += clock64() - w3t0, w3t0 = clock64()
+#define W3T_DECL uint64_t w3c[6] = {0, 0, 0, 0, 0, 0}, w3t0 = clock64(); uint32_t w3n = 0
+#define W3T_PRINT                                                                                               \
+    if (tid == 0 && blockIdx.x % 64 == 0)                                                                       \
+        printf("W3PROF blk %u runs %u hist %llu bases %llu sort %llu chain %llu stats %llu\n", blockIdx.x, w3n,  \
+               (unsigned long long)w3c[0], (unsigned long long)w3c[1], (unsigned long long)w3c[2],              \
+               (unsigned long long)w3c[3], (unsigned long long)w3c[4])
+#else
+#define W3T(i)
+#define W3T_DECL
+#define W3T_PRINT
+#endif
 // LDS: acc[m] x {found, stale, share, rate} u64 (workgroup sums), then per wave: hist F[m], stale S[m],
 // sorted candidate keys (block, slot) and their (end, flags), per-(phase, lane) bases.
 __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a, const WideOut out)
@@ -326,7 +341,12 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
     for (uint32_t i = tid; i < 4 * m; i += 256) acc[i] = 0;
     __syncthreads();
     const int64_t D = a.D;
+    W3T_DECL;
     for (uint32_t r = blockIdx.x * 4 + w; r < a.n; r += gridDim.x * 4) {  // wave-uniform loop
+#if defined(W3_PROF) && W3_PROF
+        ++w3n;
+        w3t0 = clock64();
+#endif
         const uint32_t *inf = a.info + (size_t)r * 4;
         const uint32_t n_end = inf[0], lastf = inf[1], cc = inf[2], rerr = inf[3];
         bool ok = rerr == 0;
@@ -334,6 +354,7 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             F[k] = a.hist[(size_t)r * m + k];
             S[k] = 0;
         }
+        W3T(0);
         // sorted position of every candidate: (phase, lane) base + rank within the lane
         const WideLane *lanes = a.lanes + (size_t)r * nph * 64;
         uint32_t run_total = 0;
@@ -345,6 +366,7 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
         }
         if (run_total != cc) ok = false;  // overflowed list (also flagged by W1)
         wave_sync();
+        W3T(1);
         if (ok) {
             for (uint32_t c = lane; c < cc; c += 64) {
                 const WideCand &e = a.cand[(size_t)r * a.rcap + c];
@@ -358,6 +380,7 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             }
         }
         wave_sync();
+        W3T(2);
         // chain the episodes whose first block is reached quiet: 64 sorted entries at a time go into the
         // lanes' registers, a wave-uniform walk reads them with v_readlane (no LDS round trip per step) and
         // sets a 64-bit mask of the applied ones, then those lanes apply their sparse deltas (LDS atomics)
@@ -369,31 +392,69 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             const uint32_t kb = valid ? KB[i] : 0xFFFFFFFFu, ke = valid ? KE[i] : 0u, kf = valid ? KF[i] : 0u;
             const uint32_t lim = (cc - base0) < 64 ? (cc - base0) : 64;
             uint64_t applied = 0;
-            for (uint32_t j = 0; j < lim; ++j) {
-                const uint32_t sblk = (uint32_t)__builtin_amdgcn_readlane((int)kb, (int)j);
-                if (sblk >= n_end) {
-                    stop = true;
-                    break;
-                }
-                if (sblk < cursor) continue;
-                const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)kf, (int)j) >> 16;
-                if (fl & (WREC_ERR | WREC_SKIP | WREC_RETRY)) {
+            // Fast path (the usual case at small rho): no candidate of the batch starts inside the episode
+            // before it, so every candidate before the end of the run applies, up to the first that ended the
+            // run: one ballot instead of the walk below.
+            const bool in = valid && kb < n_end;  // a prefix of the lanes (the keys are sorted)
+            const uint32_t prev_ke = (uint32_t)__shfl_up((int)ke, 1, 64);
+            const bool ovl = in && kb < (lane == 0 ? cursor : prev_ke);
+            if (__ballot(ovl) == 0ull) {
+                const uint64_t inm = __ballot(in);
+                const uint32_t fl = kf >> 16;
+                const uint64_t endm = __ballot(in && (fl & WREC_ENDED));
+                const uint64_t am = endm ? inm & (((endm & (0ull - endm)) << 1) - 1ull) : inm;
+                if (__ballot(in && (fl & (WREC_ERR | WREC_SKIP | WREC_RETRY))) & am) {
                     ok = false;
                     stop = true;
-                    break;
+                } else {
+                    applied = am;
+                    if (am) cursor = (uint32_t)__builtin_amdgcn_readlane((int)ke, 63 - __clzll((long long)am));
+                    if (endm) {
+                        run_ended = true;
+                        stop = true;
+                    } else if (inm != __ballot(valid)) {
+                        stop = true;  // a candidate at or past the end of the run
+                    }
                 }
-                applied |= 1ull << j;
-                cursor = (uint32_t)__builtin_amdgcn_readlane((int)ke, (int)j);
-                if (fl & WREC_ENDED) {
-                    run_ended = true;
-                    stop = true;
-                    break;
+            } else {
+                for (uint32_t j = 0; j < lim; ++j) {
+                    const uint32_t sblk = (uint32_t)__builtin_amdgcn_readlane((int)kb, (int)j);
+                    if (sblk >= n_end) {
+                        stop = true;
+                        break;
+                    }
+                    if (sblk < cursor) continue;
+                    const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)kf, (int)j) >> 16;
+                    if (fl & (WREC_ERR | WREC_SKIP | WREC_RETRY)) {
+                        ok = false;
+                        stop = true;
+                        break;
+                    }
+                    applied |= 1ull << j;
+                    cursor = (uint32_t)__builtin_amdgcn_readlane((int)ke, (int)j);
+                    if (fl & WREC_ENDED) {
+                        run_ended = true;
+                        stop = true;
+                        break;
+                    }
                 }
             }
             if (ok && ((applied >> lane) & 1ull)) {
+                // the record's first entries are loaded with its count, not after it
                 const uint32_t *rec = a.recs + ((size_t)r * a.rcap + (kf & 0xFFFFu)) * WREC_WORDS;
+                constexpr uint32_t PRE = 4;
+                uint32_t pre[3 * PRE];
+#pragma unroll
+                for (uint32_t q = 0; q < 3 * PRE; ++q) pre[q] = rec[4 + q];
                 const uint32_t ne = rec[2];
-                for (uint32_t q = 0; q < ne; ++q) {
+#pragma unroll
+                for (uint32_t q = 0; q < PRE; ++q) {
+                    if (q < ne) {
+                        atomicAdd(&F[pre[3 * q]], pre[3 * q + 1]);
+                        atomicAdd(&S[pre[3 * q]], pre[3 * q + 2]);
+                    }
+                }
+                for (uint32_t q = PRE; q < ne; ++q) {
                     const uint32_t g = rec[4 + 3 * q];
                     atomicAdd(&F[g], rec[5 + 3 * q]);
                     atomicAdd(&S[g], rec[6 + 3 * q]);
@@ -406,6 +467,7 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             if (a.tlast[r] + a.prop[lastf] > D) F[lastf] -= 1u;
         }
         wave_sync();
+        W3T(3);
         if (!ok) {
             if (lane == 0) atomicAdd(out.fail, 1u);
             continue;
@@ -434,7 +496,9 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
             atomicAdd(&acc[4 * k + 3], (unsigned long long)rfx);
         }
         if (out.best_h && lane == 0) out.best_h[rel] = Lp;
+        W3T(4);
     }
+    W3T_PRINT;
     __syncthreads();
     // flush: msim_sums {found, stale, share_hi, share_lo, rate_hi, rate_lo}; the workgroup's Q32.32 sums
     // are split into 2^32 and 2^0 limbs (the represented value sum(hi) + sum(lo) * 2^-32 is exact).
