@@ -46,8 +46,19 @@ constexpr uint32_t WIDE_MAX_M = 4096;   // LDS histogram of 4 waves: 64 KiB; buc
 constexpr int WB_BITS = 12;
 constexpr uint32_t WB_N = 1u << WB_BITS;  // pick buckets
 constexpr uint32_t WIDE_ST = 16;        // tail blocks per lane per chunk
-constexpr int WE_FAST = 12, WA_FAST = 6;  // episode capacities (blocks, miners that found one): first pass
-constexpr int WE = 48;                     // ... retry pass (the record format holds WA entries)
+// Episode capacities (blocks, miners that found one) of W2's two passes: every candidate with the small ones
+// (its arrays fit in registers at 104 VGPRs, 4 waves per SIMD), the ones that outgrew them with the record
+// format's full WA entries. Measured on configs[4] (profiles/r04/w2v, w2v3): first pass with 12 / 6 1.43 ms,
+// 8 / 4 0.94 ms, 6 / 3 0.78 ms per launch, retry pass 0.09-0.14 ms; a middle pass (12 / 6) between them cost
+// more than it saved.
+#ifndef MSIM_WE_FAST
+#define MSIM_WE_FAST 6
+#endif
+#ifndef MSIM_WA_FAST
+#define MSIM_WA_FAST 3
+#endif
+constexpr int WE_FAST = MSIM_WE_FAST, WA_FAST = MSIM_WA_FAST;
+constexpr int WE = 48;
 constexpr int WA = 16;
 constexpr uint32_t WREC_WORDS = 4 + 3 * WA;
 constexpr uint32_t WIDE_NONE = 0xFFFFFFFFu;
@@ -366,7 +377,9 @@ MSIM_HDN void wide_episode(const int64_t *__restrict__ prop, uint32_t m, int64_t
     o.flags = (ended ? WREC_ENDED : 0u) | (err ? WREC_ERR : 0u);
     o.ne = err ? 0u : (uint32_t)na;
     if (err) return;
-    for (int a = 0; a < na; ++a) {
+#pragma unroll
+    for (int a = 0; a < CA; ++a) {  // static indices into o: its arrays stay in registers
+        if (a >= na) continue;
         uint32_t inch = 0;
         for (int b = best; b >= 0; b = par[b]) inch += own[b] == gid[a] ? 1u : 0u;
         o.gid[a] = gid[a];

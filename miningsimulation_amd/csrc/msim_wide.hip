@@ -262,6 +262,8 @@ __global__ __launch_bounds__(64 * RUNS) __attribute__((amdgpu_waves_per_eu(W1_WA
 }
 
 // ---------------------------------------------------------------- W2
+// RETRY = false: every candidate with the small capacities (WE_FAST, WA_FAST); an episode that outgrows them is
+// listed for RETRY = true (the record format's WE, WA).
 template <bool RETRY>
 __device__ __forceinline__ void wide_episode_slot(const WideArgs &a, uint32_t slot)
 {
@@ -280,34 +282,32 @@ __device__ __forceinline__ void wide_episode_slot(const WideArgs &a, uint32_t sl
     const int64_t Ts = (int64_t)(ln.t0 + e.offset);
     WideSrc src{e.ri, e.rp, a.logt, a.cf, a.bucket, a.W, a.mult};
     WideEpOut o;
-    if (RETRY) {
-        wide_episode<WE, WA>(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
-        if (o.flags & WREC_RETRY) o.flags = WREC_ERR;
-    } else {
-        wide_episode<WE_FAST, WA_FAST>(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
-        if (o.flags & WREC_RETRY) a.retry[atomicAdd(&a.counts[1], 1u)] = slot;
+    constexpr int CE = RETRY ? WE : WE_FAST, CA = RETRY ? WA : WA_FAST;
+    wide_episode<CE, CA>(a.prop, a.m, a.D, e.block, Ts, e.f, e.inext, e.fnext, src, o);
+    if (o.flags & WREC_RETRY) {
+        if (RETRY) o.flags = WREC_ERR;
+        else a.retry[atomicAdd(&a.counts[1], 1u)] = slot;
     }
     rec[0] = o.end;
     rec[1] = o.flags;
     rec[2] = o.ne;
-    for (uint32_t i = 0; i < o.ne; ++i) {
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)CA; ++i) {  // static indices: o stays in registers
+        if (i >= o.ne) continue;
         rec[4 + 3 * i] = o.gid[i];
         rec[5 + 3 * i] = o.dF[i];
         rec[6 + 3 * i] = o.dS[i];
     }
 }
 
-// RETRY = false: every candidate with small capacities (WE_FAST, WA_FAST); RETRY = true: only the
-// candidates the first pass flagged WREC_RETRY, with the record format's full capacities.
 // Grid-stride over the dense lists W1 / the first pass built (every thread of a wave has real work).
 template <bool RETRY>
 __global__ __launch_bounds__(256) void msim_wide_episode_kernel(const WideArgs a)
 {
     const uint32_t total = RETRY ? a.counts[1] : a.counts[0];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
-        const uint32_t slot = RETRY ? a.retry[i] : a.work[i];
-        wide_episode_slot<RETRY>(a, slot);
-    }
+    const uint32_t *list = RETRY ? a.retry : a.work;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256)
+        wide_episode_slot<RETRY>(a, list[i]);
 }
 
 // ---------------------------------------------------------------- W3

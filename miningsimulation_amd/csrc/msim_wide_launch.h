@@ -89,7 +89,7 @@ inline WideLayout wide_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     L.retry_off = o;
     o = al(o + (size_t)L.nr * L.rcap * 4);
     L.counts_off = o;
-    o = al(o + 8);
+    o = al(o + 16);
     L.total = o;
     return L;
 }
