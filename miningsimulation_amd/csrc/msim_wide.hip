@@ -350,19 +350,39 @@ __global__ __launch_bounds__(256) void msim_wide_combine_kernel(const WideArgs a
         const uint32_t *inf = a.info + (size_t)r * 4;
         const uint32_t n_end = inf[0], lastf = inf[1], cc = inf[2], rerr = inf[3];
         bool ok = rerr == 0;
-        for (uint32_t k = lane; k < m; k += 64) {
-            F[k] = a.hist[(size_t)r * m + k];
-            S[k] = 0;
+        {  // the run's histogram, HB loads per lane in flight together (clamped, unconditional), then stored
+            constexpr uint32_t HB = 8;
+            const uint32_t *h = a.hist + (size_t)r * m;
+            for (uint32_t k0 = lane; k0 < m; k0 += 64 * HB) {
+                uint32_t v[HB];
+#pragma unroll
+                for (uint32_t j = 0; j < HB; ++j) v[j] = h[k0 + 64 * j < m ? k0 + 64 * j : m - 1];
+#pragma unroll
+                for (uint32_t j = 0; j < HB; ++j) {
+                    if (k0 + 64 * j < m) {
+                        F[k0 + 64 * j] = v[j];
+                        S[k0 + 64 * j] = 0;
+                    }
+                }
+            }
         }
         W3T(0);
         // sorted position of every candidate: (phase, lane) base + rank within the lane
         const WideLane *lanes = a.lanes + (size_t)r * nph * 64;
         uint32_t run_total = 0;
-        for (uint32_t ph = 0; ph < nph; ++ph) {
-            const uint32_t cnt = lanes[(size_t)ph * 64 + lane].count;
-            const uint32_t ex = (uint32_t)wave_excl_scan(cnt, lane);
-            base[ph * 64 + lane] = run_total + ex;
-            run_total += __shfl(ex + cnt, 63, 64);
+        constexpr uint32_t PB = 8;  // phases' counts loaded PB at a time (clamped, unconditional)
+        for (uint32_t ph0 = 0; ph0 < nph; ph0 += PB) {
+            uint32_t cv[PB];
+#pragma unroll
+            for (uint32_t j = 0; j < PB; ++j) cv[j] = lanes[(size_t)(ph0 + j < nph ? ph0 + j : nph - 1) * 64 + lane].count;
+#pragma unroll
+            for (uint32_t j = 0; j < PB; ++j) {
+                if (ph0 + j < nph) {  // wave-uniform
+                    const uint32_t ex = (uint32_t)wave_excl_scan(cv[j], lane);
+                    base[(ph0 + j) * 64 + lane] = run_total + ex;
+                    run_total += __shfl(ex + cv[j], 63, 64);
+                }
+            }
         }
         if (run_total != cc) ok = false;  // overflowed list (also flagged by W1)
         wave_sync();
