@@ -399,7 +399,10 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 // candidates' deltas,
 // which land while the end group is redrawn. The episode chain is built from the headers without the end
 // block (the episodes are in block order, so the end only truncates it) and cut once the redraw found it.
-constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = 32, K3_SCRATCH = K3_SEG_MAX + 2 * K3_EP_MAX;
+#ifndef MSIM_K3_EP_MAX
+#define MSIM_K3_EP_MAX 32
+#endif
+constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = MSIM_K3_EP_MAX, K3_SCRATCH = K3_SEG_MAX + 2 * K3_EP_MAX;
 template <int M>
 MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M],
                          uint32_t *nsw, size_t nss)
