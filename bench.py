@@ -43,11 +43,11 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 #   valu    = SQ_INSTS_VALU (wave instructions) per launch: the counter-based VALU issue fraction is
 #             valu x 64 lanes / the kernel's live time / peak, reported beside the SURVEY 8(d) convention.
 PMC = {
-    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "fetch_kb": 23145.5 / 2, "write_kb": 924438 / 2,
+    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "fetch_kb": 23209.4 / 2, "write_kb": 930700 / 2,
                     "valu": 3.55641e9 / 2, "src": "profiles/r04/final/pmc/pmc_c2.txt"},
-    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "fetch_kb": 9.39808e6 / 2,
-                     "write_kb": 4.66729e7 / 2, "valu": 4.99608e10 / 2, "src": "profiles/r04/final/pmc/pmc_c3.txt"},
-    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "fetch_kb": 3280.38 / 2, "write_kb": 1.82865e6 / 2,
+    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "fetch_kb": 9.38307e6 / 2,
+                     "write_kb": 4.67146e7 / 2, "valu": 4.99608e10 / 2, "src": "profiles/r04/final/pmc/pmc_c3.txt"},
+    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "fetch_kb": 3217.69 / 2, "write_kb": 1.82868e6 / 2,
                     "valu": 1.07196e10 / 2, "src": "profiles/r04/final/pmc/pmc_c5.txt"},
 }
 # rocprofv3 --kernel-trace --stats summaries of the exact bench commands (default streams and --streams 1), whose
