@@ -392,13 +392,13 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 // the run's segments (later the first blocks of the candidate episodes), the candidates' record indices, and
 // their (end << 2 | ended << 1 | unusable) words.
 //
-// K3 is latency-bound (one lane per run, a fraction of a wave per SIMD): its time is the number of dependent
-// memory rounds. The reads are ordered so that independent ones share a round and the episode reads stay in
-// flight behind the end-of-run search: (1) segment sums; (2) list counts + per-owner counts; (3) slot
-// indices; (4) episode headers + super-group ends; (5) group sums; (6) the end group's records + the first
-// candidates' deltas,
-// which land while the end group is redrawn. The episode chain is built from the headers without the end
-// block (the episodes are in block order, so the end only truncates it) and cut once the redraw found it.
+// K3 is latency-bound (one lane per run, a fraction of a wave per SIMD): its time is set by its dependent
+// memory rounds and by single-wave instruction latency. The reads are ordered so that independent ones share a
+// round and the episode reads stay in flight behind the end-of-run search: (1) segment sums; (2) list counts +
+// per-owner counts; (3) slot indices; (4) episode headers + super-group ends; (5) group sums; (6) the end
+// group's records + the first candidates' deltas, which land while the end group is redrawn. The episode
+// chain is built from the headers without the end block (the episodes are in block order, so the end only
+// truncates it) and cut once the redraw found it.
 #ifndef MSIM_K3_EP_MAX
 #define MSIM_K3_EP_MAX 32  // 24: 76.8 us, 16: 99.1 us vs 67.7 us per c2 launch (more runs on the one-read-at-a-time path)
 #endif
