@@ -35,25 +35,76 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 
 
 # PMC constants of the dominant kernel per launch at the default run counts, from rocprofv3 --pmc passes of
-# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_r04_final.sh: FETCH_SIZE, WRITE_SIZE and the
-# SQ set in separate passes; files under profiles/r04/final/pmc/, values there summed over 2 launches, KB). PMC counters
-# cannot be collected inside the timed process: these are the recorded values of the same kernel.
+# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc.sh: FETCH_SIZE, WRITE_SIZE and the SQ
+# set in separate passes; the files hold values summed over the 2 launches, KB). PMC counters cannot be collected
+# inside the timed process: these are the recorded values of the same kernel, and every field computed from them
+# names its file.
 #   traffic = FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of wide reads, MI355X_MICROARCH.md §HBM)
 #             + WRITE_SIZE, bytes per launch;
 #   valu    = SQ_INSTS_VALU (wave instructions) per launch: the counter-based VALU issue fraction is
-#             valu x 64 lanes / the kernel's live time / peak, reported beside the SURVEY 8(d) convention.
+#             valu x 64 lanes / the kernel's time / peak.
+PMC_DIR = "profiles/r05/final/pmc"
 PMC = {
-    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "fetch_kb": 23209.4 / 2, "write_kb": 930700 / 2,
-                    "valu": 3.55641e9 / 2, "src": "profiles/r04/final/pmc/pmc_c2.txt"},
-    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "fetch_kb": 9.38307e6 / 2,
-                     "write_kb": 4.67146e7 / 2, "valu": 4.99608e10 / 2, "src": "profiles/r04/final/pmc/pmc_c3.txt"},
-    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "fetch_kb": 3217.69 / 2, "write_kb": 1.82868e6 / 2,
-                    "valu": 1.07196e10 / 2, "src": "profiles/r04/final/pmc/pmc_c5.txt"},
+    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "file": "pmc_c2.txt"},
+    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "file": "pmc_c3.txt"},
+    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "file": "pmc_c5.txt"},
 }
-# rocprofv3 --kernel-trace --stats summaries of the exact bench commands (default streams and --streams 1), whose
-# average duration of the dominant kernel is the file-backed counterpart of the live HIP-event time in the line.
-ROCPROF = {"c2": "profiles/r04/final/rocprof_c2_s{s}.md", "c3": "profiles/r04/final/rocprof_c3_s{s}.md",
-           "c5": "profiles/r04/final/rocprof_c5_s{s}.md"}
+# rocprofv3 --kernel-trace --stats summaries (scripts/rocprof_summary.py) of the exact bench commands: the default
+# two streams (_s0) and --streams 1 (_s1). Their "busy ms/call" column is the union of the kernel's dispatch
+# intervals per call, the file-backed counterpart of the live dominant_ms; the serial file's average is the
+# kernel alone.
+ROCPROF_DIR = "profiles/r05/final"
+KERNEL_SUBSTR = {"c1": "msim_draws_kernel", "c2": "msim_draws_kernel", "c3": "msim_sel_kernel<",
+                 "c5": "msim_wide_draws_kernel"}
+
+
+def pmc_constants(config: str, n: int) -> dict | None:
+    """{kernel, src, fetch_kb, write_kb, valu} per launch from the committed PMC file (None if absent)."""
+    ent = PMC.get((config, n))
+    if not ent:
+        return None
+    path = os.path.join(PMC_DIR, ent["file"])
+    try:
+        txt = open(os.path.join(ROOT, path)).read()
+    except OSError:
+        return None
+    # scripts/pmc_csv.py format: a header "<kernel>  dispatches=D  mean_ms=..." (D over the three passes), then
+    # "    <COUNTER>  <value summed over the launches of its pass>" lines
+    vals, cur, launches = {}, False, 2
+    for ln in txt.splitlines():
+        if not ln.startswith(" "):
+            cur = KERNEL_SUBSTR[config] in ln and not vals
+            if cur:
+                for tok in ln.split():
+                    if tok.startswith("dispatches=") and int(tok.split("=")[1]) % 3 == 0:
+                        launches = max(1, int(tok.split("=")[1]) // 3)
+            continue
+        parts = ln.split()
+        if cur and len(parts) == 2:
+            vals[parts[0]] = float(parts[1])
+    vals = {k: v / launches for k, v in vals.items()}
+    need = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU")
+    if not all(k in vals for k in need):
+        return None
+    return {"kernel": ent["kernel"], "src": path, "fetch_kb": vals["FETCH_SIZE"], "write_kb": vals["WRITE_SIZE"],
+            "valu": vals["SQ_INSTS_VALU"]}
+
+
+def rocprof_kernel_ms(config: str, streams: int) -> dict | None:
+    """{file, avg_ms, busy_ms} of the dominant kernel in the committed rocprof summary of this command."""
+    path = os.path.join(ROCPROF_DIR, f"rocprof_{config}_s{0 if streams == 2 else 1}.md")
+    try:
+        rows = open(os.path.join(ROOT, path)).read().splitlines()
+    except OSError:
+        return None
+    for ln in rows:
+        cells = [c.strip() for c in ln.strip().strip("|").split("|")]
+        if len(cells) >= 6 and KERNEL_SUBSTR.get(config, "?") in cells[0]:
+            try:
+                return {"file": path, "avg_ms": float(cells[3]), "busy_ms": float(cells[5])}
+            except ValueError:
+                return None
+    return None
 
 
 def w_blk(m: int) -> int:
@@ -264,13 +315,16 @@ def main() -> None:
     m = len(miners)
     if args.stub:
         sim = _StubSim(m)
-        stub_t = {"on": False}
+        stub_t = {"on": False, "t0": 0.0}
 
         def timing_enable(on):
             stub_t["on"] = on
+            stub_t["t0"] = time.perf_counter()
 
-        def timing_read():
-            return {"launches": args.steps, "launch_ms": 1.0 * args.steps, "draws_ms": 1.0 * args.steps}
+        def timing_read():  # stand-in kernel spans: half of the wall clock since enable
+            ms = 0.5 * (time.perf_counter() - stub_t["t0"]) * 1e3
+            return {"launches": args.steps, "launch_ms": ms, "draws_ms": ms, "engine_ms": 0.0, "draws_busy_ms": ms,
+                    "engine_busy_ms": 0.0, "launch_busy_ms": ms}
 
         def sync():
             pass
@@ -305,6 +359,7 @@ def main() -> None:
             "total": torch.zeros((m, 6), dtype=torch.int64, device=dev),
             "status": torch.zeros(2, dtype=torch.int32, device=dev),
             "fails": torch.zeros(1, dtype=torch.int64, device=dev),
+            "local": torch.zeros((m, 6), dtype=torch.int64, device=dev),  # this rank's own sums (before reduce)
         })
     sync()
 
@@ -315,6 +370,7 @@ def main() -> None:
             sim.launch(n, begin, args.seed_base, ln["sums"], ln["ws"], ln["status"], stream=ln["stream"])
             ln["fails"].add_(ln["status"][1:2].to(torch.int64))
             if world > 1:
+                ln["local"].add_(ln["sums"])
                 dist.all_reduce(ln["sums"])  # the path's only exchange: per-miner integer sums (RCCL over xGMI)
             ln["total"].add_(ln["sums"])
 
@@ -324,6 +380,7 @@ def main() -> None:
     for ln in lanes:
         ln["total"].zero_()
         ln["fails"].zero_()
+        ln["local"].zero_()
     timing_enable(True)  # HIP events on the launch stream around every launch and every K1
     if world > 1:
         dist.barrier()
@@ -338,32 +395,95 @@ def main() -> None:
     tm = timing_read()
     timing_enable(False)
     assert tm["launches"] == args.steps, tm
-    kern_ms = tm["launch_ms"] / args.steps  # all kernels of one msim_launch (K1+K2+K3+finalize)
-    k1_ms = tm["draws_ms"] / args.steps
+    kern_ms = tm["launch_ms"] / args.steps  # all kernels of one msim_launch (K1+K2+K3+finalize), per launch
+    k1_ms = tm["draws_ms"] / args.steps     # K1 / W1 per launch (span of each launch's draw kernel)
     e1_ms = tm.get("engine_ms", 0.0) / args.steps  # E1 kernels (selfish networks)
+    # busy = union of those spans over both streams / steps: the stage's share of each step's wall clock
+    k1_busy = tm.get("draws_busy_ms", 0.0) / args.steps
+    e1_busy = tm.get("engine_busy_ms", 0.0) / args.steps
     total = sum(ln["total"] for ln in lanes)
     fails = sum(ln["fails"] for ln in lanes)
-    t = torch.tensor([elapsed, kern_ms, k1_ms, e1_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kern_ms, k1_ms, e1_ms, k1_busy, e1_busy], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(fails)
-    elapsed, kern_ms, k1_ms, e1_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
+    elapsed, kern_ms, k1_ms, e1_ms, k1_busy, e1_busy = (float(x) for x in t)
     if int(fails.item()) != 0:
         raise SystemExit(f"{int(fails.item())} runs exceeded the compact state capacity")
+    rccl = None
+    if world > 1:
+        # The exchange step, checked once outside the timed region: every rank's own (pre-reduce) found counts,
+        # gathered, must add up to the all-reduced total each rank holds.
+        local_found = sum(ln["local"] for ln in lanes)[:, 0].sum().reshape(1)
+        gathered = [torch.zeros_like(local_found) for _ in range(world)]
+        dist.all_gather(gathered, local_found)
+        per_rank = [int(g.item()) for g in gathered]
+        reduced = int(total[:, 0].sum().item())
+        rccl = {"rccl_world": dist.get_world_size(), "backend": dist.get_backend(),
+                "found_allreduced": reduced, "found_per_rank": per_rank, "ok": reduced == sum(per_rank)}
+        if not rccl["ok"]:
+            raise SystemExit(f"all-reduce check failed: {rccl}")
 
     pipe = sim.pipeline_info(n)
+    ms_step = elapsed / args.steps * 1e3
     # Roofline of the dominant kernel: the draw kernel for honest networks (K1 / W1: it does every fast block's
-    # whole work), E1 for selfish ones. Its time is the live HIP-event time on the launch stream (with two
-    # streams a launch shares the GPU with the other stream's, so this duration is longer than the kernel
-    # alone; ROCPROF's summary of the same command agrees with it).
+    # whole work), E1 for selfish ones. Its time, dominant_ms, is its BUSY time per step: the union of its
+    # launches' HIP-event spans over both streams in the timed region, divided by the steps (two launches in
+    # flight on two streams count their overlap once), so it never exceeds ms_per_step. The same union per
+    # call is in the committed rocprofv3 summary of this command (rocprof_<config>_s<0|1>.md, busy ms/call).
     honest = pipe.get("uses_pipeline") in (1, 2)
-    dom_ms = k1_ms if honest and k1_ms > 0 else (e1_ms if e1_ms > 0 else kern_ms)
-    pmc = PMC.get((args.config, n))
-    issue_frac = None
+    if honest and k1_ms > 0:
+        dom_ms, dom_span = k1_busy, k1_ms
+    elif e1_ms > 0:
+        dom_ms, dom_span = e1_busy, e1_ms
+    else:
+        dom_ms, dom_span = min(kern_ms, ms_step), kern_ms
+    pmc = None if args.stub else pmc_constants(args.config, n)
+    rp_here = rocprof_kernel_ms(args.config, ns)  # this command's summary (default streams or --streams 1)
+    rp_serial = rocprof_kernel_ms(args.config, 1)
+    peak = VALU_PEAK_LANE_OPS
+    work = n * BLOCKS_PER_RUN_YEAR * w_blk(m)  # SURVEY 8(d) convention, lane-ops per launch
+    roof = {
+        "bound": "valu",
+        "unit": "T lane-op/s",
+        "peak": round(peak / 1e12, 2),
+        "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 2.4 GHz (a wave64 VALU op issues over 2 cycles)",
+        "kernel": ("W1 msim_wide_draws_kernel" if sim.wide else "K1 msim_draws_kernel" if honest else
+                   "E1 msim_sel_kernel (settled form + entity engine)"),
+        "dominant_ms": round(dom_ms, 4),
+        "dominant_ms_how": "busy time per step: union of the kernel's HIP-event spans over the streams / steps",
+        "dominant_span_ms": round(dom_span, 4),
+        "dominant_ms_file": rp_here["file"] if rp_here else None,
+        "dominant_ms_file_busy": rp_here["busy_ms"] if rp_here else None,
+    }
     if pmc and dom_ms > 0:
-        issue_frac = round(pmc["valu"] * 64 / (dom_ms / 1e3) / VALU_PEAK_LANE_OPS, 4)
-    per_gpu_kernel_rate = n / (dom_ms / 1e3)  # run-years/s of the dominant kernel on one GPU
-    achieved = per_gpu_kernel_rate * BLOCKS_PER_RUN_YEAR * w_blk(m)  # algorithmic lane-ops/s per GPU
+        # headline: the counter-based VALU issue fraction, SQ_INSTS_VALU x 64 lanes over the kernel's busy time
+        achieved = pmc["valu"] * 64 / (dom_ms / 1e3)
+        roof.update({
+            "achieved": round(achieved / 1e12, 4),
+            "frac": round(achieved / peak, 4),
+            "frac_how": f"SQ_INSTS_VALU {pmc['valu']:.5g} per launch ({pmc['src']}) x 64 / dominant_ms / peak",
+            "traffic": round(pmc["fetch_kb"] * 1024 * 2 + pmc["write_kb"] * 1024),
+            "traffic_source": f"rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of {pmc['kernel']} per launch ({pmc['src']})",
+            "valu_per_block": round(pmc["valu"] * 64 / (n * BLOCKS_PER_RUN_YEAR), 2),
+        })
+        if rp_serial:
+            roof.update({
+                "frac_serial": round(pmc["valu"] * 64 / (rp_serial["avg_ms"] / 1e3) / peak, 4),
+                "frac_serial_how": f"same counter over the kernel alone: avg ms in {rp_serial['file']} (--streams 1)",
+            })
+    else:
+        roof.update({"achieved": None, "frac": None, "traffic": None,
+                     "frac_how": "no PMC file for this config / run count (profiles/r05/final/pmc)"})
+    # SURVEY 8(d)'s fixed accounting (156 lane-ops per block at M = 9): saturated, because K1 skips the state
+    # machine for >99.9 % of blocks; kept for continuity, never the headline.
+    roof["frac_convention_per_step"] = round(work / (ms_step / 1e3) / peak, 4)
+    roof["saturated"] = roof["frac_convention_per_step"] >= 0.95
+    if rp_serial:
+        roof["frac_convention_serial"] = round(work / (rp_serial["avg_ms"] / 1e3) / peak, 4)
+    roof["accounting"] = f"SURVEY 8(d): W_blk({m}) = {w_blk(m)} lane-ops/block x 52594.92 blocks/run-year"
+    roof["kernel_ms"] = round(kern_ms, 4)
+    roof["pipeline"] = pipe
     runs_total = args.steps * n * world
     value = runs_total / elapsed
     # sanity: aggregate share of miner 0 (integer sums, exact across ranks)
@@ -378,14 +498,15 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64+fp64",
             "data": "synthetic (seeded runs; run r uses rd()-equivalents (base+2r, base+2r+1))",
             "config": {
-                "workload": {"c2": "c2: BASELINE configs[1]", "c3": "c3: BASELINE configs[2]",
+                "workload": {"c1": "c1: BASELINE configs[0] (10 s propagation)", "c2": "c2: BASELINE configs[1]",
+                             "c3": "c3: BASELINE configs[2]",
                              "c5": "c5: BASELINE configs[4] (SURVEY Appendix C weights, W=102400)"}.get(args.config, args.config),
                 "network": ([[mm.id, mm.perc, mm.propagation_ms, int(mm.is_selfish)] for mm in miners] if m <= 16 else
                             f"{m} miners: weights 30720, 29696, 1024 x 41 (W=102400), all honest, prop 1000 ms"),
@@ -395,30 +516,10 @@ def main() -> None:
                                f"steps alternate over {ns} HIP stream(s)",
                 "miner0_share_pct": round(share0, 5),
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved / 1e12, 4),
-                "peak": round(VALU_PEAK_LANE_OPS / 1e12, 2),
-                "unit": "T lane-op/s",
-                "frac": round(achieved / VALU_PEAK_LANE_OPS, 5),
-                "traffic": round(pmc["fetch_kb"] * 1024 * 2 + pmc["write_kb"] * 1024) if pmc else None,
-                "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of {pmc['kernel']} per launch "
-                                   f"(serial bench, {pmc['src']})") if pmc else None,
-                "valu_issue_frac_pmc": issue_frac,
-                "valu_issue_source": (f"SQ_INSTS_VALU {pmc['valu']:.4g} per launch ({pmc['src']}) x 64 lanes / "
-                                      f"dominant_ms / peak") if pmc else None,
-                "kernel": ("W1 msim_wide_draws_kernel" if sim.wide else "K1 msim_draws_kernel" if honest else
-                           "E1 msim_sel_kernel (settled form + entity engine)") + " (HIP events on the launch stream)",
-                "dominant_ms": round(dom_ms, 4),
-                "dominant_ms_file": ROCPROF[args.config].format(s=0 if ns == 2 else 1)
-                if args.config in ROCPROF and ns in (1, 2) and args.steps == 40 else None,
-                "kernel_ms": round(kern_ms, 4),
-                "k1_ms": round(k1_ms, 4),
-                "k1_share": round(k1_ms / kern_ms, 4) if kern_ms > 0 else None,
-                "pipeline": pipe,
-                "accounting": f"SURVEY 8(d): W_blk({m}) = {w_blk(m)} lane-ops/block x 52594.92 blocks/run-year",
-            },
+            "roofline": roof,
         }
+        if rccl:
+            line["rccl"] = rccl
         if args.stub:
             line["data"] = "STUB (--stub: CPU stand-in for the launch, tests of the rank/JSON plumbing only)"
         if world == 1 and not args.no_cpu_baseline and not args.stub:

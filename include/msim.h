@@ -119,6 +119,17 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
  * msim_run for every n_devices (out_sums from the fixed-point sums; opt_sums or NULL). */
 int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
                    const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums);
+/* msim_run_multi plus per-device timing: opt_shard_ms (2 * n_devices doubles or NULL) receives, for device g,
+ * [2g] the milliseconds of its shard's launches and [2g + 1] those of the all-reduce that follows them
+ * (HIP events on the device's stream), so a host can see how evenly the shards ran. */
+int msim_run_multi_timed(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
+                         const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums,
+                         double *opt_shard_ms);
+/* Lifetime of the cached communicators of msim_run_multi / msim_sweep_run_multi: one set per device list,
+ * created on first use and kept for the process. msim_multi_release destroys every set no call is using and
+ * returns how many it released (a host that cycles through many device lists, or that resets its devices,
+ * calls it first). A set whose collectives fail is destroyed at once and re-created by the next call. */
+int msim_multi_release(void);
 
 /* Device-resident launch on the current HIP device and the given hipStream_t (NULL = default).
  * d_sums: M msim_sums in device memory (overwritten). d_per_run / d_best_height: device buffers or NULL.
@@ -177,6 +188,15 @@ int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches);
 /* Same, plus the entity engine's stage (networks with selfish miners: the E1 kernels of every slice;
  * draws_ms is then the word-draw kernel D1). */
 int msim_timing_read_stages(double *draws_ms, double *engine_ms, double *launch_ms, uint32_t *launches);
+/* Same, plus BUSY time: the union of the stage's (begin, end) intervals over every stream, i.e. how long at
+ * least one such kernel was running (two launches in flight on two streams count their overlap once). With
+ * launches alternating over streams this is the stage's share of the wall clock, never more than it. */
+typedef struct msim_timing {
+    double draws_ms, engine_ms, launch_ms;                 /* summed per-launch intervals */
+    double draws_busy_ms, engine_busy_ms, launch_busy_ms;  /* union of the intervals */
+    uint32_t launches;
+} msim_timing;
+int msim_timing_read_all(msim_timing *out);
 
 /* How msim_launch will execute n_runs of this config on the current device. */
 typedef struct msim_pipeline_layout {

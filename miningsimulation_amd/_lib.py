@@ -32,6 +32,8 @@ EXPORTED = (
     "msim_config_miner_count",
     "msim_run",
     "msim_run_multi",
+    "msim_run_multi_timed",
+    "msim_multi_release",
     "msim_sweep_run_multi",
     "msim_sweep_point_count",
     "msim_sweep_miner_count",
@@ -44,6 +46,7 @@ EXPORTED = (
     "msim_timing_enable",
     "msim_timing_read",
     "msim_timing_read_stages",
+    "msim_timing_read_all",
     "msim_pipeline_info",
     "msim_sweep_create",
     "msim_sweep_destroy",
@@ -55,6 +58,12 @@ EXPORTED = (
     "msim_sample_picks",
     "msim_sample_intervals",
 )
+
+
+class MsimTiming(ctypes.Structure):
+    _fields_ = [("draws_ms", ctypes.c_double), ("engine_ms", ctypes.c_double), ("launch_ms", ctypes.c_double),
+                ("draws_busy_ms", ctypes.c_double), ("engine_busy_ms", ctypes.c_double),
+                ("launch_busy_ms", ctypes.c_double), ("launches", ctypes.c_uint32)]
 
 
 class MsimMiner(ctypes.Structure):
@@ -132,6 +141,12 @@ def _load() -> ctypes.CDLL:
     lib.msim_run_multi.argtypes = [vp, u64, u64, u32, ctypes.POINTER(ctypes.c_int), u32, ctypes.POINTER(MsimStats),
                                    ctypes.POINTER(MsimSums)]
     lib.msim_run_multi.restype = ctypes.c_int
+    lib.msim_run_multi_timed.argtypes = [vp, u64, u64, u32, ctypes.POINTER(ctypes.c_int), u32,
+                                         ctypes.POINTER(MsimStats), ctypes.POINTER(MsimSums),
+                                         ctypes.POINTER(ctypes.c_double)]
+    lib.msim_run_multi_timed.restype = ctypes.c_int
+    lib.msim_multi_release.argtypes = []
+    lib.msim_multi_release.restype = ctypes.c_int
     lib.msim_sweep_run_multi.argtypes = [vp, u64, u64, u32, ctypes.POINTER(ctypes.c_int), u32,
                                          ctypes.POINTER(MsimStats), ctypes.POINTER(MsimSums)]
     lib.msim_sweep_run_multi.restype = ctypes.c_int
@@ -159,6 +174,8 @@ def _load() -> ctypes.CDLL:
     lib.msim_timing_read_stages.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u32)]
     lib.msim_timing_read_stages.restype = ctypes.c_int
+    lib.msim_timing_read_all.argtypes = [ctypes.POINTER(MsimTiming)]
+    lib.msim_timing_read_all.restype = ctypes.c_int
     lib.msim_pipeline_info.argtypes = [vp, u64, ctypes.POINTER(MsimPipelineLayout)]
     lib.msim_pipeline_info.restype = ctypes.c_int
     lib.msim_sweep_create.argtypes = [ctypes.POINTER(vp), u32, ctypes.POINTER(vp)]

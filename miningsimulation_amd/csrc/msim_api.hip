@@ -1343,6 +1343,52 @@ int msim_timing_read_stages(double *draws_ms, double *engine_ms, double *launch_
     return rc;
 }
 
+// Union length of (begin, end) event pairs: every event timed against the first begin (same device), the
+// intervals sorted and merged.
+static int busy_ms(const std::vector<hipEvent_t> &v, double *out)
+{
+    *out = 0;
+    if (v.size() < 2) return MSIM_OK;
+    std::vector<std::pair<double, double>> iv;
+    for (size_t i = 0; i + 1 < v.size(); i += 2) {
+        float a = 0, b = 0;
+        if (hipEventSynchronize(v[i + 1]) != hipSuccess || hipEventElapsedTime(&a, v[0], v[i]) != hipSuccess ||
+            hipEventElapsedTime(&b, v[0], v[i + 1]) != hipSuccess)
+            return MSIM_E_HIP;
+        iv.emplace_back(a, b);
+    }
+    std::sort(iv.begin(), iv.end());
+    double lo = iv[0].first, hi = iv[0].second, acc = 0;
+    for (const auto &p : iv) {
+        if (p.first > hi) {
+            acc += hi - lo;
+            lo = p.first;
+            hi = p.second;
+        } else if (p.second > hi) {
+            hi = p.second;
+        }
+    }
+    *out = acc + (hi - lo);
+    return MSIM_OK;
+}
+
+int msim_timing_read_all(msim_timing *out)
+{
+    if (!out) return MSIM_E_INVALID;
+    memset(out, 0, sizeof(*out));
+    int rc = MSIM_OK;
+    {
+        Timing &tm = timing();
+        std::lock_guard<std::mutex> g(tm.mu);
+        const std::vector<hipEvent_t> *vs[3] = {&tm.k1, &tm.engine, &tm.launch};
+        double *busy[3] = {&out->draws_busy_ms, &out->engine_busy_ms, &out->launch_busy_ms};
+        for (int i = 0; i < 3; ++i)
+            if (busy_ms(*vs[i], busy[i]) != MSIM_OK) rc = MSIM_E_HIP;
+    }
+    const int r2 = msim_timing_read_stages(&out->draws_ms, &out->engine_ms, &out->launch_ms, &out->launches);
+    return rc ? rc : r2;
+}
+
 int msim_timing_read(double *draws_ms, double *launch_ms, uint32_t *launches)
 {
     double e = 0;

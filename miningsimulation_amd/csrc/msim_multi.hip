@@ -10,6 +10,7 @@
 // device count.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <memory>
@@ -17,6 +18,7 @@
 #include <vector>
 
 #include "../../include/msim.h"
+#include "msim_commcache.h"
 
 namespace {
 
@@ -47,6 +49,7 @@ struct Shard {
     uint32_t *d_stat = nullptr;  // [2] status of every chunk
     uint64_t *d_part = nullptr;  // [nv] one chunk's sums
     uint32_t *d_pst = nullptr;   // [2] one chunk's status
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // timing: shard start, shard done, all-reduce done
 };
 
 // What one device launches for a chunk of runs: a config (msim_launch) or a sweep (msim_sweep_launch).
@@ -73,7 +76,7 @@ struct Job {
     }
 };
 
-int alloc_shard(const Job &job, Shard &sh)
+int alloc_shard(const Job &job, Shard &sh, bool timed)
 {
     const uint32_t nv = job.nv;
     const uint64_t mc = job.max_chunk();
@@ -88,6 +91,9 @@ int alloc_shard(const Job &job, Shard &sh)
         hipMemsetAsync(sh.d_acc, 0, nv * sizeof(uint64_t), sh.s) != hipSuccess ||
         hipMemsetAsync(sh.d_stat, 0, 2 * sizeof(uint32_t), sh.s) != hipSuccess)
         return MSIM_E_HIP;
+    if (timed)
+        for (hipEvent_t &e : sh.ev)
+            if (hipEventCreate(&e) != hipSuccess) return MSIM_E_HIP;
     return MSIM_OK;
 }
 
@@ -99,6 +105,8 @@ void free_shard(Shard &sh)
     (void)hipFree(sh.d_pst);
     (void)hipFree(sh.d_acc);
     (void)hipFree(sh.d_stat);
+    for (hipEvent_t &e : sh.ev)
+        if (e) (void)hipEventDestroy(e);
     if (sh.s) (void)hipStreamDestroy(sh.s);
 }
 
@@ -109,6 +117,7 @@ void enqueue_shard(const Job &job, uint32_t seed_base, Shard &sh)
         sh.rc = MSIM_E_HIP;
         return;
     }
+    if (sh.ev[0]) (void)hipEventRecord(sh.ev[0], sh.s);
     for (uint64_t off = 0; sh.rc == MSIM_OK && off < sh.n; off += sh.chunk) {
         const uint64_t cn = (sh.n - off) < sh.chunk ? (sh.n - off) : sh.chunk;
         sh.rc = job.launch(sh.begin + off, cn, seed_base, sh.d_part, sh.d_pst, sh.ws, sh.wsb, sh.s);
@@ -117,48 +126,28 @@ void enqueue_shard(const Job &job, uint32_t seed_base, Shard &sh)
         hipLaunchKernelGGL(add_status_kernel, dim3(1), dim3(64), 0, sh.s, sh.d_stat, sh.d_pst);
         if (hipGetLastError() != hipSuccess) sh.rc = MSIM_E_HIP;
     }
+    if (sh.ev[1]) (void)hipEventRecord(sh.ev[1], sh.s);
 }
 
-// Single-process communicators, one per device list, created on first use and kept for the life of the
-// process (ncclCommInitAll costs milliseconds to seconds per call; a host driver that calls msim_run_multi
-// once per sweep point must not pay it every time). A communicator is used by one call at a time: its
-// entry's mutex is held from the first enqueue to the last synchronisation. An entry whose collectives
-// failed is dropped (destroyed) so that the next call starts from a fresh communicator.
-struct CommEntry {
-    std::vector<int> devs;
-    std::vector<ncclComm_t> comms;
-    std::mutex use;
+// Communicator cache (msim_commcache.h) over RCCL: one single-process communicator set per device list.
+struct RcclBackend {
+    using Comm = ncclComm_t;
+    static bool init(Comm *comms, int n, const int *devs) { return ncclCommInitAll(comms, n, devs) == ncclSuccess; }
+    static void destroy(Comm c) { (void)ncclCommDestroy(c); }
 };
-std::mutex g_comm_mu;
-std::vector<std::shared_ptr<CommEntry>> g_comms;
-
-std::shared_ptr<CommEntry> comm_for(const std::vector<int> &devs, int *rc)
+using Cache = msim::CommCache<RcclBackend>;
+Cache &comm_cache()
 {
-    std::lock_guard<std::mutex> g(g_comm_mu);
-    for (const auto &e : g_comms)
-        if (e->devs == devs) return e;
-    auto e = std::make_shared<CommEntry>();
-    e->devs = devs;
-    e->comms.assign(devs.size(), nullptr);
-    if (ncclCommInitAll(e->comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
-        *rc = MSIM_E_HIP;
-        return nullptr;
-    }
-    g_comms.push_back(e);
-    return e;
+    static Cache c;
+    return c;
 }
 
-void comm_drop(const std::shared_ptr<CommEntry> &e)
+// Test hook: MSIM_MULTI_FAIL_COLLECTIVE=1 makes every grouped collective report failure, so the retire path
+// runs on a real communicator set (the race itself is covered on the host: tests/native/commcache_host.cpp).
+bool forced_collective_failure()
 {
-    std::lock_guard<std::mutex> g(g_comm_mu);
-    for (size_t i = 0; i < g_comms.size(); ++i)
-        if (g_comms[i] == e) {
-            for (ncclComm_t c : e->comms)
-                if (c) (void)ncclCommDestroy(c);
-            e->comms.assign(e->comms.size(), nullptr);
-            g_comms.erase(g_comms.begin() + (long)i);
-            return;
-        }
+    const char *e = getenv("MSIM_MULTI_FAIL_COLLECTIVE");
+    return e && e[0] == '1';
 }
 
 // Shards [run_begin, run_begin + n_runs) over the devices, runs them, all-reduces; acc = reduced sums.
@@ -167,7 +156,7 @@ void comm_drop(const std::shared_ptr<CommEntry> &e)
 // multi-device form), so no device can be left waiting in a collective that another never joins: a
 // device whose launches failed contributes its (zero-initialised) buffers and the call returns its error.
 int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, const int *devices,
-            uint32_t n_devices, std::vector<uint64_t> &acc)
+            uint32_t n_devices, std::vector<uint64_t> &acc, double *opt_shard_ms)
 {
     std::vector<int> devs(n_devices);
     for (uint32_t g = 0; g < n_devices; ++g) devs[g] = devices ? devices[g] : (int)g;
@@ -183,37 +172,48 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
         sh[g].device = devs[g];
         sh[g].begin = run_begin + g * base + (g < rem ? g : rem);
         sh[g].n = base + (g < rem ? 1 : 0);
-        if (rc == MSIM_OK) rc = alloc_shard(job, sh[g]);
+        if (rc == MSIM_OK) rc = alloc_shard(job, sh[g], opt_shard_ms != nullptr);
     }
     // one device: its sums are the result (no collective)
-    std::shared_ptr<CommEntry> ce;
-    if (rc == MSIM_OK && n_devices > 1) ce = comm_for(devs, &rc);
-    std::unique_lock<std::mutex> use;
-    if (ce) use = std::unique_lock<std::mutex>(ce->use);
+    Cache::Lease ce;
+    if (rc == MSIM_OK && n_devices > 1) {
+        ce = comm_cache().acquire(devs);
+        if (!ce.ok) rc = MSIM_E_HIP;
+    }
     if (rc == MSIM_OK) {
         for (auto &x : sh) enqueue_shard(job, seed_base, x);
         bool coll_failed = false;
-        if (ce && ncclGroupStart() != ncclSuccess) {
+        if (ce.ok && (forced_collective_failure() || ncclGroupStart() != ncclSuccess)) {
             rc = MSIM_E_HIP;
             coll_failed = true;
-        } else if (ce) {
+        } else if (ce.ok) {
             for (uint32_t g = 0; g < n_devices; ++g)
-                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv, ncclUint64, ncclSum, ce->comms[g], sh[g].s) != ncclSuccess ||
-                    ncclAllReduce(sh[g].d_stat, sh[g].d_stat, 2, ncclUint32, ncclSum, ce->comms[g], sh[g].s) != ncclSuccess)
+                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv, ncclUint64, ncclSum, ce.e->comms[g], sh[g].s) != ncclSuccess ||
+                    ncclAllReduce(sh[g].d_stat, sh[g].d_stat, 2, ncclUint32, ncclSum, ce.e->comms[g], sh[g].s) != ncclSuccess)
                     rc = MSIM_E_HIP;
             if (ncclGroupEnd() != ncclSuccess) rc = MSIM_E_HIP;
             coll_failed = rc != MSIM_OK;
         }
         for (auto &x : sh)
+            if (x.ev[2]) (void)hipEventRecord(x.ev[2], x.s);
+        for (auto &x : sh)
             if (hipSetDevice(x.device) != hipSuccess || hipStreamSynchronize(x.s) != hipSuccess) rc = rc ? rc : MSIM_E_HIP;
         for (const auto &x : sh)
             if (x.rc) rc = rc ? rc : x.rc;
-        if (coll_failed) {
-            if (use.owns_lock()) use.unlock();
-            comm_drop(ce);
+        if (coll_failed) comm_cache().retire(ce);  // under the entry's lock (msim_commcache.h)
+    }
+    if (ce.lock.owns_lock()) ce.lock.unlock();
+    if (opt_shard_ms) {  // per device: its launches, and the all-reduce after them
+        for (uint32_t g = 0; g < n_devices; ++g) {
+            float a = 0, b = 0;
+            if (rc == MSIM_OK && (hipSetDevice(sh[g].device) != hipSuccess ||
+                                  hipEventElapsedTime(&a, sh[g].ev[0], sh[g].ev[1]) != hipSuccess ||
+                                  hipEventElapsedTime(&b, sh[g].ev[1], sh[g].ev[2]) != hipSuccess))
+                rc = MSIM_E_HIP;
+            opt_shard_ms[2 * g] = a;
+            opt_shard_ms[2 * g + 1] = b;
         }
     }
-    if (use.owns_lock()) use.unlock();
     acc.assign(job.nv, 0);
     uint32_t st[2] = {0, 0};
     if (rc == MSIM_OK) {  // every device holds the reduced sums: read the first one's
@@ -230,18 +230,25 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
 
 }  // namespace
 
-extern "C" int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
-                              const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums)
+extern "C" int msim_run_multi_timed(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
+                                    const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums,
+                                    double *opt_shard_ms)
 {
     if (!cfg || !out_sums || n_runs == 0 || n_devices == 0 || n_devices > 64) return MSIM_E_INVALID;
     const uint32_t m = msim_config_miner_count(cfg);
     std::vector<uint64_t> acc;
-    const int rc = run_job(Job{cfg, nullptr, 6 * m}, run_begin, n_runs, seed_base, devices, n_devices, acc);
+    const int rc = run_job(Job{cfg, nullptr, 6 * m}, run_begin, n_runs, seed_base, devices, n_devices, acc, opt_shard_ms);
     if (rc) return rc;
     const msim_sums *fs = (const msim_sums *)acc.data();
     if (opt_sums) memcpy(opt_sums, fs, sizeof(msim_sums) * m);
     msim_sums_to_stats(fs, m, out_sums);
     return MSIM_OK;
+}
+
+extern "C" int msim_run_multi(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base,
+                              const int *devices, uint32_t n_devices, msim_stats *out_sums, msim_sums *opt_sums)
+{
+    return msim_run_multi_timed(cfg, run_begin, n_runs, seed_base, devices, n_devices, out_sums, opt_sums, nullptr);
 }
 
 extern "C" int msim_sweep_run_multi(const msim_sweep *sweep, uint64_t run_begin, uint64_t runs_per_point,
@@ -251,10 +258,13 @@ extern "C" int msim_sweep_run_multi(const msim_sweep *sweep, uint64_t run_begin,
     if (!sweep || !out_stats || runs_per_point == 0 || n_devices == 0 || n_devices > 64) return MSIM_E_INVALID;
     const uint32_t nv = 6 * msim_sweep_miner_count(sweep) * msim_sweep_point_count(sweep);
     std::vector<uint64_t> acc;
-    const int rc = run_job(Job{nullptr, sweep, nv}, run_begin, runs_per_point, seed_base, devices, n_devices, acc);
+    const int rc =
+        run_job(Job{nullptr, sweep, nv}, run_begin, runs_per_point, seed_base, devices, n_devices, acc, nullptr);
     if (rc) return rc;
     const msim_sums *fs = (const msim_sums *)acc.data();
     if (opt_sums) memcpy(opt_sums, fs, sizeof(uint64_t) * nv);
     msim_sums_to_stats(fs, nv / 6, out_stats);
     return MSIM_OK;
 }
+
+extern "C" int msim_multi_release(void) { return comm_cache().release(); }

@@ -20,7 +20,7 @@ from typing import Iterable, List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import MsimMiner, MsimRunRecord, MsimStats, MsimSums, check, lib
+from ._lib import MsimMiner, MsimRunRecord, MsimStats, MsimSums, MsimTiming, check, lib
 
 SIM_DURATION_MS = 31_556_952_000  # main.cpp:7 std::chrono::months{12}
 SIM_RUNS = 16 * 2048              # main.cpp:10
@@ -174,12 +174,15 @@ class Simulation:
         stats = (MsimStats * m)()
         sums = (MsimSums * m)()
         devs = (ctypes.c_int * len(devices))(*devices)
-        check(lib.msim_run_multi(self._h, run_begin, n_runs, seed_base & 0xFFFFFFFF, devs, len(devices), stats, sums),
-              "msim_run_multi")
+        shard_ms = (ctypes.c_double * (2 * len(devices)))()
+        check(lib.msim_run_multi_timed(self._h, run_begin, n_runs, seed_base & 0xFFFFFFFF, devs, len(devices), stats,
+                                       sums, shard_ms), "msim_run_multi_timed")
         return SimulationResult(
             stats_total=[MinerStats(s.blocks_found, s.blocks_share, s.stale_rate) for s in stats],
             sums=list(sums),
             n_runs=n_runs,
+            # per device: [launches ms, all-reduce ms] (msim_run_multi_timed)
+            extra={"shard_ms": [(shard_ms[2 * g], shard_ms[2 * g + 1]) for g in range(len(devices))]},
         )
 
     def pipeline_info(self, n_runs: int) -> dict:
@@ -311,11 +314,12 @@ def timing_enable(on: bool = True) -> None:
 
 def timing_read() -> dict:
     """Summed draw-kernel / entity-engine / whole-launch milliseconds and the launch count since the last
-    enable/read (synchronises). draws_ms: K1 / W1 (honest pipelines; 0 for selfish networks); engine_ms: E1."""
-    d, e, l, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
-    check(lib.msim_timing_read_stages(ctypes.byref(d), ctypes.byref(e), ctypes.byref(l), ctypes.byref(n)),
-          "msim_timing_read_stages")
-    return {"draws_ms": d.value, "engine_ms": e.value, "launch_ms": l.value, "launches": n.value}
+    enable/read (synchronises). draws_ms: K1 / W1 (honest pipelines; 0 for selfish networks); engine_ms: E1.
+    *_busy_ms: the union of those intervals over every stream (msim_timing_read_all): the stage's share of the
+    wall clock when launches overlap on several streams."""
+    t = MsimTiming()
+    check(lib.msim_timing_read_all(ctypes.byref(t)), "msim_timing_read_all")
+    return {k: getattr(t, k) for k, _ in MsimTiming._fields_}
 
 
 def sums_to_stats(sums_rows: Iterable[Sequence[int]]) -> List[MinerStats]:

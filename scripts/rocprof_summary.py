@@ -1,4 +1,11 @@
-"""Summarise a rocprofv3 --kernel-trace --stats output (SQLite .db or *_kernel_stats.csv) as a table."""
+"""Summarise a rocprofv3 --kernel-trace --stats output (SQLite .db or *_kernel_stats.csv) as a table.
+
+Columns: calls, total and average duration, share of kernel time, and "busy ms/call": the union of the
+kernel's dispatch intervals divided by its calls. With launches alternating over two HIP streams two
+dispatches of one kernel overlap; the union counts that overlap once, so busy ms/call is the kernel's share
+of the wall clock per launch (bench.py's live dominant_ms is the same quantity from HIP events). Needs the
+.db form (per-dispatch start/end); the CSV form prints the average there.
+"""
 import csv
 import glob
 import os
@@ -6,25 +13,44 @@ import sqlite3
 import sys
 
 
+def union_ms(iv):
+    iv = sorted(iv)
+    acc, lo, hi = 0, None, None
+    for a, b in iv:
+        if hi is None or a > hi:
+            if hi is not None:
+                acc += hi - lo
+            lo, hi = a, b
+        elif b > hi:
+            hi = b
+    if hi is not None:
+        acc += hi - lo
+    return acc / 1e6  # ns -> ms
+
+
 def main(path: str) -> None:
     dbs = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
     rows = []
     if dbs:
         c = sqlite3.connect(dbs[0])
+        spans = {}
+        for name, a, b in c.execute("select name, start, end from kernels"):
+            spans.setdefault(name, []).append((a, b))
+        busy = {name: union_ms(iv) / len(iv) for name, iv in spans.items()}
         # the rocpd top_kernels view reports microseconds
-        rows = [(n, k, t * 1e3, a * 1e3, p) for n, k, t, a, p in
+        rows = [(n, k, t * 1e3, a * 1e3, p, busy.get(n, a * 1e-3)) for n, k, t, a, p in
                 c.execute("select name, total_calls, total_duration, average, percentage from top_kernels")]
     else:
         for f in glob.glob(os.path.join(path, "**", "*kernel_stats.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
                     rows.append((r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]),
-                                 float(r["Percentage"])))
-    print("| kernel | calls | total ms | avg ms | % |")
-    print("|---|---|---|---|---|")
-    for name, calls, tot, avg, pct in rows:
+                                 float(r["Percentage"]), float(r["AverageNs"]) / 1e6))
+    print("| kernel | calls | total ms | avg ms | % | busy ms/call |")
+    print("|---|---|---|---|---|---|")
+    for name, calls, tot, avg, pct, bz in rows:
         short = name.split("(")[0][:90]
-        print(f"| `{short}` | {calls} | {tot / 1e6:.3f} | {avg / 1e6:.4f} | {pct:.2f} |")
+        print(f"| `{short}` | {calls} | {tot / 1e6:.3f} | {avg / 1e6:.4f} | {pct:.2f} | {bz:.4f} |")
 
 
 if __name__ == "__main__":

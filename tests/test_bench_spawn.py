@@ -29,12 +29,28 @@ def test_spawn_two_ranks_one_line():
     assert d["data"].startswith("STUB")
     # whole-job aggregate: 2 ranks x 3 steps x 32768 runs over the max-over-ranks time
     assert abs(d["value"] * d["ms_per_step"] * 3 / 1e3 - 2 * 3 * 32768) < 1e-3 * 2 * 3 * 32768
+    _check_rccl(d, 2)
+
+
+def _check_rccl(d, n):
+    """The line shows the collective saw every rank: world size, and the all-reduced found count equals the
+    sum of each rank's own counts gathered once outside the timed region."""
+    r = d["rccl"]
+    assert r["rccl_world"] == n
+    assert r["ok"] is True
+    assert len(r["found_per_rank"]) == n
+    assert r["found_allreduced"] == sum(r["found_per_rank"])
+    assert all(v > 0 for v in r["found_per_rank"])
 
 
 def test_single_rank_unchanged():
     d = _bench("--gpus", "1", "--steps", "2", "--warmup", "0")
     assert d["n_gpus"] == 1
     assert "cpu_baseline" not in d
+    assert "rccl" not in d
+    # no time in the roofline exceeds the step (the dominant kernel's busy time is a share of the step)
+    roof = d["roofline"]
+    assert roof["dominant_ms"] <= d["ms_per_step"] + 1e-9
 
 
 def test_spawn_eight_ranks():
@@ -42,6 +58,7 @@ def test_spawn_eight_ranks():
     d = _bench("--gpus", "8", "--steps", "2", "--warmup", "1")
     assert d["n_gpus"] == 8
     assert abs(d["value"] * d["ms_per_step"] * 2 / 1e3 - 8 * 2 * 32768) < 1e-3 * 8 * 2 * 32768
+    _check_rccl(d, 8)
 
 
 def test_spawn_failing_rank_ends_job():
