@@ -203,7 +203,9 @@ typedef struct msim_pipeline_layout {
     uint32_t uses_pipeline;   /* 1: event-skipping pipeline (honest network); 2: large-network pipeline;
                                  3: entity engine (selfish miners); 4: general engine (slice_runs = its
                                  lanes, segment_blocks = its first window, segments = window tiers,
-                                 blocks_per_run = its last window); 0: per-lane kernel */
+                                 blocks_per_run = its last window); 5: selfish pipeline (one selfish miner:
+                                 draw kernel + settled form from finder nibbles, rho = its candidate rate);
+                                 0: per-lane kernel */
     uint32_t slice_runs;      /* runs per pipeline slice */
     uint32_t segment_blocks;  /* blocks per draw-kernel worker */
     uint32_t segments;        /* workers per run */

@@ -59,6 +59,7 @@ constexpr uint32_t K1_NSL = K1_OWNERS;         // LDS row after the owners: the 
 // budget (K1_WAVES below) goes to the draws. Measured on MI355X (profiles/r03/INDEX.md): with the lane id,
 // its bit, the list count and the counter address held across the loop, the compiler reloaded them from
 // scratch once per quad (six scratch loads and two vmcnt(0) waits per quad).
+template <bool NIB>
 struct DevCtx {
     const DrawArgs &a;
     uint32_t (*cnt)[256];
@@ -66,6 +67,7 @@ struct DevCtx {
     uint32_t tid, r0, seg, jb;  // r0: the wave's first run (wave-uniform)
     uint32_t cbase;             // tid * 4, rebuilt every quad (quad())
     uint32_t wbase;             // 4 x the wave's first thread (SGPR)
+    uint32_t nibw;              // NIB: the finders of the last 8 blocks, oldest in the low nibble
     __device__ __forceinline__ void quad()
     {
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshl_add_u32 %0, %0, 2, %1"
@@ -78,10 +80,25 @@ struct DevCtx {
         const uint32_t ad = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)&cnt[0][0] +
                             ((info & (15u << INFO_K_SHIFT)) | cbase);
         __atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)ad, 1u, __ATOMIC_RELAXED);
+        if (NIB) nibw = (nibw >> 4) | ((info & (15u << INFO_K_SHIFT)) << (28 - INFO_K_SHIFT));
+    }
+    // NIB: one u32 of 8 finder nibbles per 8 blocks, [word][run] (a wave stores 256 contiguous bytes)
+    __device__ __forceinline__ void quad_done(uint32_t g, uint32_t q4)
+    {
+        if (NIB && (q4 & 1u)) a.nib[((size_t)seg * (a.seg / 8) + g * (GROUP / 8) + (q4 >> 1)) * a.nr + run()] = nibw;
     }
     __device__ __forceinline__ bool vote(bool s) const { return (__builtin_amdgcn_ballot_w64(s) & amask) != 0ull; }
     // the owner counters packed as the u16 pairs of the workspace layout (msim_pipeline.h CNT_WORDS)
     __device__ __forceinline__ uint32_t packed(uint32_t w) const { return cnt[2 * w][tid] | (cnt[2 * w + 1][tid] << 16); }
+    // The wave's reserved chunk of the episode list, [lend - lleft, lend) still free (wave-uniform).
+    uint32_t lend, lleft;
+    // Mark the unused tail of the wave's chunk (K2 skips EP_HOLE slots; no run's slots point there).
+    __device__ void holes()
+    {
+        uint32_t lane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=&v"(lane));
+        if (lane < lleft && lend - lleft + lane < a.lcap) a.list[lend - lleft + lane].run = EP_HOLE;
+    }
     __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         const uint64_t mask = __builtin_amdgcn_ballot_w64(s) & amask;
@@ -89,9 +106,18 @@ struct DevCtx {
         uint32_t below;
         asm volatile("v_mbcnt_lo_u32_b32 %0, %1, 0\n\tv_mbcnt_hi_u32_b32 %0, %2, %0"
                      : "=&v"(below) : "s"((uint32_t)mask), "s"((uint32_t)(mask >> 32)));
-        uint32_t base = 0;
-        if (s & (below == 0u)) base = atomicAdd(a.list_count, (uint32_t)__popcll(mask));
-        base = __builtin_amdgcn_readlane(base, (uint32_t)(__ffsll((unsigned long long)mask) - 1));
+        const uint32_t nsel = (uint32_t)__popcll(mask);
+        if (nsel > lleft) {  // wave-uniform: a new chunk (the old one's tail becomes holes)
+            holes();
+            const uint32_t need = nsel > a.lchunk ? nsel : a.lchunk;
+            uint32_t base = 0;
+            if (s & (below == 0u)) base = atomicAdd(a.list_count, need);
+            base = __builtin_amdgcn_readlane(base, (uint32_t)(__ffsll((unsigned long long)mask) - 1));
+            lend = base + need;
+            lleft = need;
+        }
+        const uint32_t base = lend - lleft;
+        lleft -= nsel;
         if (!s) return;
         uint32_t lane;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=&v"(lane));
@@ -145,6 +171,9 @@ struct DevCtx {
 #ifndef MSIM_K1_WAVES
 #define MSIM_K1_WAVES 6
 #endif
+// NIB: the selfish pipeline's K1 (msim_selpipe.h): every block's finder nibble stored, a block listed when
+// I_{i+1} < fthr (STRICT; its table gives honest finders fthr = prop_k + prop_s + 1, selfish ones 0).
+template <bool NIB>
 #if MSIM_K1_WAVES
 __global__ __launch_bounds__(256, MSIM_K1_WAVES) void msim_draws_kernel(const DrawArgs a)
 #else
@@ -173,10 +202,11 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
 
     const uint32_t b0 = seg * a.seg;
-    DevCtx cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, (uint32_t)__builtin_amdgcn_readfirstlane(r & ~63u), seg,
-              seg - a.band_lo, 0u,
-              (uint32_t)__builtin_amdgcn_readfirstlane((tid & ~63u) * 4u)};
-    const uint64_t tsum = draw_segment(cx, ri, rp, &sm.log, &sm.pick, b0, a.seg, seg >= a.band_lo);
+    DevCtx<NIB> cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, (uint32_t)__builtin_amdgcn_readfirstlane(r & ~63u), seg,
+                   seg - a.band_lo, 0u,
+                   (uint32_t)__builtin_amdgcn_readfirstlane((tid & ~63u) * 4u), 0u, 0u, 0u};
+    const uint64_t tsum = draw_segment<DevCtx<NIB>, NIB>(cx, ri, rp, &sm.log, &sm.pick, b0, a.seg, seg >= a.band_lo);
+    cx.holes();
     a.segsum[(size_t)seg * a.nr + r] = tsum;
 #pragma unroll
     for (uint32_t w = 0; w < CNT_WORDS; ++w) a.segcnt[((size_t)seg * CNT_WORDS + w) * a.nr + r] = cx.packed(w);
@@ -218,12 +248,13 @@ hipError_t launch_picks(const PickTab *pt, const uint64_t *u, int32_t *out, uint
 
 hipError_t draws_blocks_per_cu(int *blocks)
 {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_draws_kernel, 256, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_draws_kernel<false>, 256, 0);
 }
 
 hipError_t launch_draws(const DrawArgs &a, hipStream_t s)
 {
-    hipLaunchKernelGGL(msim_draws_kernel, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
+    if (a.nib) hipLaunchKernelGGL(msim_draws_kernel<true>, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(msim_draws_kernel<false>, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

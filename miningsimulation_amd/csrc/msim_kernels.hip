@@ -301,6 +301,8 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.cap = L.cap;
     da.band_lo = L.band_lo;
     da.lcap = L.lcap;
+    da.lchunk = L.lchunk;
+    da.nib = nullptr;
     da.segsum = (uint64_t *)(ws + L.segsum_off);
     da.segcnt = (uint32_t *)(ws + L.segcnt_off);
     da.nslow = (uint32_t *)(ws + L.nslow_off);

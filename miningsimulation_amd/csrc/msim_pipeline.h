@@ -46,8 +46,10 @@ constexpr uint32_t CNT_WORDS = 8;       // per-owner counters packed as u16 pair
 #endif
 constexpr int K1_QB = MSIM_K1_QB;
 
+constexpr uint32_t EP_HOLE = 0xFFFFFFFFu;  // EpEntry::run of a list slot K1 reserved but did not use
+
 struct EpEntry {
-    uint32_t run;     // slice-local run
+    uint32_t run;     // slice-local run (EP_HOLE: an unused slot of a wave's reserved chunk)
     uint32_t block;   // block index within the run
     uint64_t offset;  // T_block - (start time of its segment), ms
     uint32_t w0, w1;  // (interval << 5 | finder) of the block and of the next one
@@ -73,6 +75,7 @@ struct PipeLayout {
     uint32_t band_lo;  // first segment with group metadata (where the run can end)
     uint32_t nband;
     uint32_t lcap;     // episode list capacity
+    uint32_t lchunk;   // list slots a K1 wave reserves at a time (one atomic per chunk, not per append)
     uint32_t rec_words;
     uint32_t k2_lean;  // K2 runs the lean state machine (rho <= K2_LEAN_RHO)
     size_t segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gend_off, gcum_off, grec_off, list_off, recs_off,
@@ -91,7 +94,7 @@ struct DrawArgs {
     uint64_t run_begin;   // absolute index of the slice's first run
     uint32_t n;           // valid runs in the slice
     uint32_t seed_base;
-    uint32_t nr, seg, gps, nseg, cap, band_lo, lcap;
+    uint32_t nr, seg, gps, nseg, cap, band_lo, lcap, lchunk;
     uint64_t *segsum;     // [nseg][nr]
     uint32_t *segcnt;     // [nseg][8][nr]
     uint32_t *nslow;      // [nseg][nr]
@@ -102,6 +105,7 @@ struct DrawArgs {
     GroupRec *grec;       // [nband][gps][nr]
     EpEntry *list;        // [lcap]
     uint32_t *list_count;
+    uint32_t *nib;        // selfish pipeline only: [nb / 8][nr] finder nibbles, block 8w + i in bits 4i..4i+3
 };
 
 struct PipeArgs {  // K2 / K3
@@ -175,7 +179,14 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     const double lam = rho * L.seg;
     L.cap = (uint32_t)ceil(lam + 8.0 * sqrt(lam) + 8.0);
     const double ent = (double)L.nr * rho * L.nb;
-    L.lcap = (uint32_t)ceil(ent + 8.0 * sqrt(ent) + 1024.0);
+    // A K1 wave reserves list slots a chunk at a time: one same-address atomic per chunk instead of one per
+    // append (at rho = 1.7 % — configs[0] — the per-append atomics serialised K1 to 56x its draw time). The
+    // chunk follows a wave's expected appends; its unused tail (< lchunk slots per wave) is marked EP_HOLE.
+    const double per_wave = 64.0 * rho * L.seg;
+    L.lchunk = 16;
+    while (L.lchunk < 256 && L.lchunk < per_wave / 4.0) L.lchunk *= 2;
+    const double holes = (double)(L.nr / 64) * L.nseg * L.lchunk;
+    L.lcap = (uint32_t)ceil(ent + 8.0 * sqrt(ent) + 1024.0 + holes);
     size_t o = 0;
     L.segsum_off = o;
     o = al(o + (size_t)L.nseg * L.nr * 8);
@@ -288,12 +299,16 @@ MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, cons
 //   group(g, sum, end)                band only: sum of the group's intervals, and the time from the segment's
 //                                     start to the group's end
 //   quad()                            start of a quad of blocks
+//   quad_done(g, q4)                  after quad q4 of group g (the selfish pipeline's K1 stores its finder
+//                                     nibbles here, msim_selpipe.h; a no-op for honest networks)
 //   group_start(g, w0, ri, rp)        band only: before group g's first block (its word and the streams
 //                                     after it; snapshot the counters)
+// STRICT: a block is listed when I_{i+1} < fthr (the selfish pipeline, whose table gives selfish finders
+// fthr = 0: never listed) instead of I_{i+1} <= fthr (honest networks: fthr = the finder's delay).
 // Blocks are drawn four at a time (draw_quad_fast); the streams after a block inside a quad, needed only
 // by the rare non-fast block, are re-stepped from the quad's start. Time is summed per group in 32 bits
 // (32 intervals < 2^25 ms each) and folded into 64 bits per group.
-template <class Ctx>
+template <class Ctx, bool STRICT = false>
 MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restrict__ lt,
                               const PickTab *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
 {
@@ -334,7 +349,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
 #pragma unroll
             for (int q = 0; q < K1_QB; ++q) {
                 gacc += Icur;
-                const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
+                const bool slow = STRICT ? I[q] < info_fthr(infocur) : I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
                 cx.count(infocur);
                 if (cx.vote(slow)) {
                     Rng a = ri0, b = rp0;  // the streams after block i+1
@@ -348,6 +363,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
                 Icur = I[q];
                 infocur = info[q];
             }
+            cx.quad_done(g, q4);
         }
         if (band) cx.group(g, gacc, tsum + gacc);
         tsum += gacc;
@@ -743,6 +759,7 @@ template <int M, bool LEAN>
 MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
 {
     const EpEntry e = a.list[idx];
+    if (e.run == EP_HOLE) return;  // never referenced by a run's slots
     uint32_t *rec = a.recs + (size_t)idx * a.rec_words;
     rec[2 + 2 * M] = e.block;
     const uint32_t seg = e.block / a.seg;

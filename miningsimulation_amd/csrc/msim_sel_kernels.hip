@@ -7,6 +7,7 @@
 #include "msim_reduce.h"
 #include "msim_sel_launch.h"
 #include "msim_selm.h"
+#include "msim_selpipe.h"
 
 namespace msim {
 
@@ -457,6 +458,181 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 #endif
 }
 
+// S2 of the selfish pipeline (msim_selpipe.h): one lane per run of the slice, one network (point 0). The
+// lane applies the settled-state transition from K1's finder nibbles (the nibble phase, all lanes a word at
+// a time) until a candidate needs the engine or the run reaches B; such lanes wait, and when xth of them wait
+// (or no lane is left in the nibble phase) the wave runs an engine phase: each waiting lane is seeded from K1's
+// stored RNG states (sp_enter) and stepped by the entity engine until it hands its run back to the nibble
+// phase (take_back below B) or finishes. The settled state and the nibble cursor wait in LDS during engine phases, so they
+// and the engine's registers are never live together.
+template <int M, bool UNI>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_selpipe_kernel(const SelArgs a,
+                                                                                                            const SpArgs sa)
+{
+    __shared__ uint32_t s_cnt[4 * M][TPB];
+    __shared__ uint32_t s_mc[SelMacro<M>::NW][TPB];
+    __shared__ uint32_t s_cur[SpCur::NW][TPB];
+    __shared__ int64_t s_prop[MAXM];
+    __shared__ uint8_t s_lut[128];
+    __shared__ LogTab s_log[1];
+    const uint32_t tid = threadIdx.x;
+    const SelParams *P = a.pts;
+    if (tid < MAXM) s_prop[tid] = P->prop[tid];
+    if (tid < 128) {
+        uint32_t f = 0;
+        for (int j = 0; j < MAXM; ++j) f += P->ccum[j] <= tid ? 1u : 0u;
+        s_lut[tid] = (uint8_t)f;
+    }
+    if (tid < LOG_TAB) {
+        s_log[0].invc[tid] = a.logt->invc[tid];
+        s_log[0].A[tid] = a.logt->A[tid];
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
+    __syncthreads();
+    const uint32_t lr = blockIdx.x * TPB + tid;  // run of the slice (K1's slice-local index)
+    const bool active = lr < a.sn;
+    const uint32_t rel = a.s0 + lr;
+    SelDevEnv<M, UNI> env{&s_cnt[0][tid], s_prop, P->prop[0], P->uniform_prop != 0, a.cold + (size_t)blockIdx.x * TPB + tid,
+                          a.cold_lanes};
+    const int64_t D = P->duration_ms;
+    const uint32_t sid = P->sids[0];
+    int64_t thr = 0;
+    for (uint32_t k = 0; k < P->m; ++k)
+        if (k != sid) thr = P->prop[k] + P->prop[sid] > thr ? P->prop[k] + P->prop[sid] : thr;
+    const int xth = (int)__builtin_amdgcn_readfirstlane(P->xth >= 1u && P->xth <= 64u ? P->xth : (uint32_t)SEL_XTH);
+    uint32_t *mcs = &s_mc[0][tid], *cs = &s_cur[0][tid];
+    // the lane's exact drawer (B's group redrawn in the prologue and at an engine entry at B), made where it is used
+    auto drawer = [&]() {
+        SelFastDraw<M> d;
+        d.lt = s_log;
+        d.lut = s_lut;
+        d.P = P;
+        d.kc = fd_consts();
+        d.wt = false;
+        return d;
+    };
+    SpCur cur;
+    SelMacro<M> mc;
+    int mode = 3;
+    uint32_t bh = 0, err = 0;
+    if (active) {
+        SelFastDraw<M> drw = drawer();
+        sp_begin(sa, lr, D, thr, drw, cur);
+        mc.F = mc.h = mc.w = mc.sst = mc.Ff = 0;
+        mc.T = 0;
+        mc.k = 0;
+#pragma unroll
+        for (int i = 0; i < SelMacro<M>::NP; ++i) mc.pend[i] = mc.stp[i] = 0;
+        err = cur.err | (a.force_retry ? SERR_CAP : 0u);
+        mode = err ? 3 : 0;
+    }
+    auto park = [&](const SelOut &r) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            env.set(C_F, (uint32_t)k, r.found[k]);
+            env.set(C_S, (uint32_t)k, r.stale[k]);
+        }
+        bh = r.best_height;
+        err |= r.err;
+    };
+    auto vote = [](bool b) { return __builtin_amdgcn_ballot_w64(b) != 0ull; };
+    for (;;) {
+        const uint64_t bn = __builtin_amdgcn_ballot_w64(mode == 0);
+        const uint64_t bw = __builtin_amdgcn_ballot_w64((mode == 1) | (mode == 4));
+        if ((bn | bw) == 0ull) break;
+        if (bw != 0ull && (__builtin_popcountll(bw) >= xth || bn == 0ull)) {
+            mc.save(mcs, TPB);
+            cur.save(cs, TPB);
+            Sel<M, 1, 1, 4, 1, SEL_NC> s;
+            SpSrc<SelFifo<SelFastDraw<M>>, SelDevEnv<M, UNI>> src;
+            src.f.d = drawer();
+            src.f.n = 0;
+            src.env = env;
+            src.pidx = SP_NONE;
+            src.pk = 0;
+            src.B = cur.B;
+            if ((mode == 1) | (mode == 4)) {
+                mode = sp_enter<M>(sa, lr, mode, cur, mc, src, s, env, P->m, P->sids);
+                if (mode == 3) err |= cur.err;
+            }
+            for (;;) {
+                if (mode == 2) {
+                    const bool live = s.step(env, src, D);
+                    if (!live) {
+                        SelOut r;
+                        s.finish(env, D, r);
+                        park(r);
+                        mode = 3;
+                    } else if (src.pidx < src.B) {
+                        SelMacro<M> tb;
+                        if (tb.take_back(env, s, sid)) {  // back to the nibble form at src.pidx (sp_seek below)
+                            tb.save(mcs, TPB);
+                            cs[0] = src.pidx;  // SpCur::pos
+                            mode = 7;
+                        }
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(mode == 2) == 0ull) break;
+            }
+            mc.load(mcs, TPB);
+            cur.load(cs, TPB);
+            if (mode == 7) {
+                sp_seek(sa, lr, cur, cur.pos);
+                mode = cur.err ? 3 : 0;
+                err |= cur.err;
+            }
+        } else {
+            for (;;) {
+                if (mode == 0) {
+                    mode = sp_word<M>(sa, lr, env, vote, cur, mc, sid, D);
+                    if (mode == 6) {
+                        SelOut r;
+                        mc.finish(env, sid, r);
+                        park(r);
+                        mode = 3;
+                    }
+                    if (mode == 3) err |= cur.err;
+                }
+                if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
+                    __builtin_popcountll(__builtin_amdgcn_ballot_w64((mode == 1) | (mode == 4))) >= xth)
+                    break;
+            }
+        }
+    }
+    SelOut o;
+    o.err = err;
+    o.best_height = bh;
+    if (active && !err) {
+        uint32_t F[M];
+        sp_counts<M>(sa, lr, cur, F);
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            o.found[k] = env.get(C_F, (uint32_t)k) + F[k];
+            o.stale[k] = env.get(C_S, (uint32_t)k);
+        }
+    }
+    uint64_t v[6 * M];
+#pragma unroll
+    for (int i = 0; i < 6 * M; ++i) v[i] = 0;
+    if (active) {
+        if (o.err) {
+            const uint32_t pos = atomicAdd(a.counts, 1u);
+            if (pos < a.err_cap) a.err_list[pos] = rel;
+        } else {
+            sel_terms<M>(o, v);
+            if (a.records)
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    a.records[2 * ((size_t)rel * M + k) + 0] = o.found[k];
+                    a.records[2 * ((size_t)rel * M + k) + 1] = o.stale[k];
+                }
+            if (a.best_h) a.best_h[rel] = o.best_height;
+        }
+    }
+    block_reduce_store<M>(v, a.partials + ((size_t)a.s0 / TPB + blockIdx.x) * 6 * M);
+}
+
 // E2: one lane per flagged (point, run), wide capacities, draws from the seeds.
 template <int M, int NS>
 __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
@@ -541,6 +717,13 @@ hipError_t MSIM_CAT(launch_sel_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, h
 #else
     return hipErrorInvalidValue;
 #endif
+}
+hipError_t MSIM_CAT(launch_selpipe_m, MSIM_M)(const SelArgs &a, const SpArgs &sa, hipStream_t s)
+{
+    const dim3 grid((a.sn + TPB - 1) / TPB);
+    if (a.uni) hipLaunchKernelGGL((msim_selpipe_kernel<MSIM_M, true>), grid, dim3(TPB), 0, s, a, sa);
+    else hipLaunchKernelGGL((msim_selpipe_kernel<MSIM_M, false>), grid, dim3(TPB), 0, s, a, sa);
+    return hipGetLastError();
 }
 hipError_t MSIM_CAT(launch_sel_retry_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, hipStream_t s)
 {

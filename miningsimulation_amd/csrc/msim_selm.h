@@ -186,23 +186,11 @@ struct SelMacro {
         return true;
     }
 
-    // One find. Returns 0 (next find pending), 1 (this find needs the entity engine), 2 (run over: the
-    // next find is at or after D). src.spec() lets a source that draws in-lane produce a later draw that
-    // does not depend on this step's outcome, so its arithmetic overlaps the transition below.
-    template <class Env, class Src>
-    MSIM_HD int step(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
+    // The settled-state transition of a find by miner k (is_s: k is the selfish miner), applied only when ok
+    // (branch-free: every update is masked). It touches no counter: found blocks are counted by the caller
+    // (step: one provisional count per find; the selfish pipeline: by its draw kernel, msim_selpipe.h).
+    MSIM_HD void transition(uint32_t k, bool is_s, bool ok, uint32_t sid)
     {
-        const int64_t pk = env.prop_tab(k < (uint32_t)M ? k : 0u);  // read before the draw's table reads
-        src.spec();
-        uint32_t I = 0, kn = 0;
-        const bool have = src.peek(I, kn);
-        const bool is_s = k == sid;
-        const int64_t thr = is_s ? 0 : pk + (w != 0u ? ps : 0);
-        // (F - Ff bounds the honest stale blocks added to stp since the last flush: a lane about to reach
-        // 2^16 takes the engine path, whose hand-over flushes)
-        const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (F - Ff < 0xFF00u) &
-                        (is_s | (((int64_t)I > thr) & (T + thr < D)));
-        // Branch-free: a lane that needs the engine applies nothing (every update below is masked by ok).
         const bool hon = ok & !is_s;
         const bool sf = ok & is_s;
         const bool res = hon & (w == 0u);     // the honest branch wins (h == 0: a plain honest block)
@@ -219,6 +207,25 @@ struct SelMacro {
         w = sf ? w + 1u : (rs ? 0u : w - (tie ? 1u : 0u));
 #pragma unroll
         for (int i = 0; i < NP; ++i) pend[i] = rs ? 0ull : pend[i];
+    }
+
+    // One find. Returns 0 (next find pending), 1 (this find needs the entity engine), 2 (run over: the
+    // next find is at or after D). src.spec() lets a source that draws in-lane produce a later draw that
+    // does not depend on this step's outcome, so its arithmetic overlaps the transition below.
+    template <class Env, class Src>
+    MSIM_HD int step(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
+    {
+        const int64_t pk = env.prop_tab(k < (uint32_t)M ? k : 0u);  // read before the draw's table reads
+        src.spec();
+        uint32_t I = 0, kn = 0;
+        const bool have = src.peek(I, kn);
+        const bool is_s = k == sid;
+        const int64_t thr = is_s ? 0 : pk + (w != 0u ? ps : 0);
+        // (F - Ff bounds the honest stale blocks added to stp since the last flush: a lane about to reach
+        // 2^16 takes the engine path, whose hand-over flushes)
+        const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (F - Ff < 0xFF00u) &
+                        (is_s | (((int64_t)I > thr) & (T + thr < D)));
+        transition(k, is_s, ok, sid);
         env.add(C_F, k < (uint32_t)M ? k : 0u, ok ? 1u : 0u);
         src.spec_b();  // the speculative draw is completed in I2 / k2 before pop_if can shift it
         src.spec_fix();

@@ -47,11 +47,12 @@ def native_tests():
     wide = os.path.join(ROOT, "build", "libwide_host.so")
     sel = os.path.join(ROOT, "build", "libsel_host.so")
     gen = os.path.join(ROOT, "build", "libgeneral_host.so")
-    outs = (lib, chk, pipe, wide, sel, gen)
+    sp = os.path.join(ROOT, "build", "libselpipe_host.so")
+    outs = (lib, chk, pipe, wide, sel, gen, sp)
     if not all(os.path.exists(p) for p in outs) or _stale(outs):
         ge.build_native_tests()
     return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel,
-            "general_host": gen}
+            "general_host": gen, "selpipe_host": sp}
 
 
 @pytest.fixture(scope="session")

@@ -86,3 +86,15 @@ def test_gpu_run_sharded_side_stream_many_chunks(msim, preset):
     st = torch.cuda.Stream()
     got = run_sharded(sim, n, 1000, run_begin=123, stream=st, max_chunk=1024).cpu().tolist()
     assert got == _rows(sim.run(n, 123, 1000, 0).sums)
+
+
+def test_gpu_run_multi_shard_timing_and_release(msim):
+    """msim_run_multi_timed reports each device's launch and all-reduce milliseconds (HIP events on its stream);
+    msim_multi_release frees cached communicators (none exist for one device)."""
+    from miningsimulation_amd._lib import lib
+
+    sim = msim.Simulation(msim.PRESETS["c2"]())
+    r = sim.run_multi(4096, 0, 1000, devices=[0])
+    (launch_ms, reduce_ms), = r.extra["shard_ms"]
+    assert launch_ms > 0.0 and reduce_ms >= 0.0
+    assert lib.msim_multi_release() == 0
