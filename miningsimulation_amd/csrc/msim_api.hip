@@ -89,6 +89,7 @@ struct msim_config {
     // wide combine cannot hold.
     GenHost gh;
     bool general = false;
+    bool selfish = false;  // some miner is selfish (G's window tiers, msim_general_launch.h gen_tiers)
     std::vector<std::pair<int, void *>> gtables;  // per device: GenParams + arrays
 };
 
@@ -381,7 +382,7 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
     w.cold_lanes = e1 > w.err_cap ? e1 : (size_t)w.err_cap;
     w.cold_off = al(w.list_off + (size_t)w.err_cap * 4);
     w.gen_off = al(w.cold_off + w.cold_lanes * msim::SEL_NC * sizeof(msim::ColdAct));
-    w.g = msim::gen_ws_layout(m, duration_ms, w.err_cap, GEN_FALLBACK_BUDGET);
+    w.g = msim::gen_ws_layout(m, duration_ms, w.err_cap, GEN_FALLBACK_BUDGET, true);
     w.total = al(w.gen_off + w.g.total);
     return w;
 }
@@ -432,6 +433,7 @@ struct SpPlan {
     msim::SpLayout SL;
     msim::PipeTables tab;
     char *ws;
+    uint32_t ps;  // the selfish miner's delay (K1's never-settles mask bit)
 };
 
 // The slice loop of one launch: E1 per group (or, for a network the selfish pipeline serves, K1<NIB> + S2 per
@@ -504,10 +506,11 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
         da.list = (EpEntry *)(pw + L.list_off);
         da.list_count = (uint32_t *)(pw + L.count_off);
         da.nib = (uint32_t *)(pw + sp->SL.nib_off);
+        da.cmask = (CMask *)(pw + sp->SL.cmask_off);
+        da.ps = sp->ps;
         SpArgs sa;
         sa.nr = L.nr;
         sa.seg = L.seg;
-        sa.gps = L.gps;
         sa.nsg = L.nsg;
         sa.nseg = L.nseg;
         sa.nb = L.nb;
@@ -518,12 +521,12 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
         sa.segcnt = da.segcnt;
         sa.nslow = da.nslow;
         sa.slots = da.slots;
-        sa.gsum = da.gsum;
         sa.gend = da.gend;
         sa.gcum = da.gcum;
         sa.grec = da.grec;
         sa.list = da.list;
         sa.nib = da.nib;
+        sa.cmask = da.cmask;
         a.plist = groups[0].plist;
         a.nlist = 1;
         a.uni = groups[0].uni;
@@ -652,10 +655,10 @@ struct GenOnlyWs {
     msim::GenWs g;
     size_t gen_off, total;
 };
-GenOnlyWs gen_only_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
+GenOnlyWs gen_only_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms, bool selfish)
 {
     GenOnlyWs w;
-    w.g = msim::gen_ws_layout(m, duration_ms, (uint32_t)(rpp * np), GEN_BUDGET);
+    w.g = msim::gen_ws_layout(m, duration_ms, (uint32_t)(rpp * np), GEN_BUDGET, selfish);
     w.gen_off = 256;
     w.total = w.gen_off + w.g.total;
     return w;
@@ -752,7 +755,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     const bool gen = nself > (uint32_t)msim::SEL_MAXS || (nself && n > MSIM_MAX_MINERS) || id_quirk ||
                      n > msim::WIDE_MAX_M || getenv("MSIM_FORCE_GENERAL") != nullptr;
     // G holds every miner's explicit chain: one lane of its last window must fit (msim_general_launch.h).
-    if (gen && !msim::gen_fits(n, duration_ms)) return MSIM_E_MINERS;
+    if (gen && !msim::gen_fits(n, duration_ms, nself > 0)) return MSIM_E_MINERS;
     const bool sel = nself > 0 && !gen;
     const bool narrow = n <= MSIM_MAX_MINERS && (total_weight == 100 || sel);
     const bool force_wide = getenv("MSIM_FORCE_WIDE") != nullptr && nself == 0;
@@ -761,6 +764,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     c->n = n;
     c->total_weight = total_weight;
     c->general = gen;
+    c->selfish = nself > 0;
     c->gh.duration_ms = duration_ms;
     c->gh.W = total_weight;
     for (uint32_t k = 0; k < n; ++k) {
@@ -812,7 +816,9 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         c->pipe_ok = !sel && !gen && prop_ok && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
         // The selfish pipeline (msim_selpipe.h): one selfish miner, the settled form (every delay >= 1 ms),
         // integer percentages (K1's pick table), rare candidates, and a run of at least ~1 000 blocks (its
-        // end search needs a band of groups).
+        // end search needs a band of groups). Opt-in (MSIM_SELPIPE=1): measured on MI355X it is still slower
+        // than E1 on configs[2] (1.90 M against 2.35 M run-years/s, profiles/r05/INDEX.md), so E1 serves by
+        // default.
         if (sel && c->sp.macro && c->sp.ns == 1 && total_weight == 100) {
             c->sp_rho = msim::sp_rho(c->perc, c->prop, c->self, (int)n);
             bool fits = true;
@@ -820,6 +826,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
             for (uint32_t k = 0; k < n; ++k)
                 fits = fits && miners[k].propagation_ms + ps + 1 < (int64_t)msim::FTHR_CAP;
             c->sp_ok = fits && c->sp_rho <= msim::SP_MAX_RHO && (double)duration_ms / 599999.5 >= 1024.0 &&
+                       getenv("MSIM_SELPIPE") != nullptr && atoi(getenv("MSIM_SELPIPE")) != 0 &&
                        getenv("MSIM_NO_SELPIPE") == nullptr;
         }
     } else {
@@ -904,7 +911,7 @@ uint32_t msim_config_miner_count(const msim_config *cfg) { return cfg ? cfg->n :
 size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
 {
     if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
-    if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total;
+    if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->selfish).total;
     if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
     if (cfg->sel)
         return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total + (cfg->sp_ok ? sp_layout(cfg, n_runs).total : 0);
@@ -919,7 +926,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
 {
     if (!cfg || !d_sums || !d_status || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
     if (cfg->general) {
-        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
+        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->selfish);
         if (workspace_bytes < w.total) return MSIM_E_INVALID;
         msim_config *c = const_cast<msim_config *>(cfg);
         const msim::GenParams *gp = nullptr;
@@ -1002,6 +1009,9 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
             rc = device_tables(c, plan.SL.L.seg, plan.SL.L.nseg, &plan.tab, 1);
             if (rc) return rc;
             plan.ws = (char *)d_workspace + w.total;
+            plan.ps = 0;
+            for (uint32_t k = 0; k < cfg->n; ++k)
+                if (cfg->self[k]) plan.ps = (uint32_t)cfg->prop[k];
         }
         rc = sel_launch_impl(cfg->n, 1, pts, gp, groups, lt, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
                              d_per_run, d_best_height, d_status, s, on ? &tm.engine : nullptr, cfg->sp_ok ? &plan : nullptr,
@@ -1202,7 +1212,7 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
             return MSIM_E_INVALID;
         }
         w->pts.push_back(cfgs[i]->p);
-        w->self = w->self || cfgs[i]->p.selfish >= 0;
+        w->self = w->self || cfgs[i]->selfish || cfgs[i]->p.selfish >= 0;
         w->sel = w->sel || cfgs[i]->sel;
         w->general = w->general || cfgs[i]->general;
         w->gens.push_back(cfgs[i]->gh);
@@ -1253,7 +1263,7 @@ uint32_t msim_sweep_miner_count(const msim_sweep *sw) { return sw ? sw->m : 0u; 
 size_t msim_sweep_workspace_bytes(const msim_sweep *sw, uint64_t runs_per_point)
 {
     if (!sw || runs_per_point == 0 || runs_per_point * sw->pts.size() > MAX_LAUNCH_RUNS) return 0;
-    if (sw->general) return gen_only_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration).total;
+    if (sw->general) return gen_only_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration, sw->self).total;
     if (sw->sel) return sel_ws_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration).total;
     return sweep_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point).total;
 }
@@ -1273,7 +1283,7 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
         const int rc = gen_cached(sm->mu, sm->gdev, hs, &gp);
         if (rc) return rc;
         if (sw->general) {
-            const GenOnlyWs w = gen_only_layout(sw->m, np, runs_per_point, sw->max_duration);
+            const GenOnlyWs w = gen_only_layout(sw->m, np, runs_per_point, sw->max_duration, sw->self);
             if (workspace_bytes < w.total) return MSIM_E_INVALID;
             return gen_launch_impl(sw->m, np, gp, w, (char *)d_workspace, run_begin, runs_per_point, seed_base, d_sums,
                                    d_per_run, d_best_height, d_status, (hipStream_t)stream);
@@ -1505,7 +1515,7 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     memset(out, 0, sizeof(*out));
     out->rho = cfg->rho;
     if (cfg->general) {
-        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
+        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->selfish);
         out->uses_pipeline = 4;
         out->slice_runs = (uint32_t)w.g.tier[0].lanes;
         out->segment_blocks = w.g.tier[0].cap;

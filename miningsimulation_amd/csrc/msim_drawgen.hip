@@ -13,6 +13,7 @@
 #include "msim_jump.h"
 #include "msim_kernels.h"
 #include "msim_pipeline.h"
+#include "msim_selpipe.h"
 
 namespace msim {
 
@@ -53,6 +54,9 @@ __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rn
 // aggregated appends to the dense episode list, the band's group records.
 constexpr uint32_t K1_OWNERS = 2 * CNT_WORDS;  // 15 miners + PickFinder's fall-through (index 15)
 constexpr uint32_t K1_NSL = K1_OWNERS;         // LDS row after the owners: the lane's slow-block count
+constexpr uint32_t K1_MA = K1_NSL + 1;         // NIB: the candidate masks of the lane's current group (A, B)
+constexpr uint32_t K1_NW = K1_MA + 2;          // NIB: the group's first three nibble words
+constexpr uint32_t K1_ROWS = K1_NW + 3;
 
 // The slow path keeps no per-lane register across the draw loop: its lane-dependent values are rebuilt from
 // the ballot mask (mbcnt), wave-uniform SGPRs and LDS (the per-lane list count), so the loop's register
@@ -82,10 +86,22 @@ struct DevCtx {
         __atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)ad, 1u, __ATOMIC_RELAXED);
         if (NIB) nibw = (nibw >> 4) | ((info & (15u << INFO_K_SHIFT)) << (28 - INFO_K_SHIFT));
     }
-    // NIB: one u32 of 8 finder nibbles per 8 blocks, [word][run] (a wave stores 256 contiguous bytes)
+    // NIB: one u32 of 8 finder nibbles per 8 blocks; a group's four words wait in LDS and leave as one 16-byte
+    // store (the chunk layout of msim_selpipe.h) with the group's candidate masks (kept in LDS by slow():
+    // nothing on the fast path)
     __device__ __forceinline__ void quad_done(uint32_t g, uint32_t q4)
     {
-        if (NIB && (q4 & 1u)) a.nib[((size_t)seg * (a.seg / 8) + g * (GROUP / 8) + (q4 >> 1)) * a.nr + run()] = nibw;
+        if (!NIB || !(q4 & 1u)) return;
+        if (q4 != GROUP / K1_QB - 1) {
+            cnt[K1_NW + (q4 >> 1)][tid] = nibw;
+            return;
+        }
+        const size_t c = (size_t)seg * (a.seg / GROUP) + g;
+        *(uint4 *)(a.nib + sp_nib_index(a.nr, run(), (uint32_t)c * 4)) =
+            make_uint4(cnt[K1_NW][tid], cnt[K1_NW + 1][tid], cnt[K1_NW + 2][tid], nibw);
+        a.cmask[c * a.nr + run()] = CMask{cnt[K1_MA][tid], cnt[K1_MA + 1][tid]};
+        cnt[K1_MA][tid] = 0;
+        cnt[K1_MA + 1][tid] = 0;
     }
     __device__ __forceinline__ bool vote(bool s) const { return (__builtin_amdgcn_ballot_w64(s) & amask) != 0ull; }
     // the owner counters packed as the u16 pairs of the workspace layout (msim_pipeline.h CNT_WORDS)
@@ -99,7 +115,8 @@ struct DevCtx {
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=&v"(lane));
         if (lane < lleft && lend - lleft + lane < a.lcap) a.list[lend - lleft + lane].run = EP_HOLE;
     }
-    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
+    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp,
+                         uint32_t fthr)
     {
         const uint64_t mask = __builtin_amdgcn_ballot_w64(s) & amask;
         // rank of this lane among the slow ones (asm volatile: computed here, not hoisted out of the loop)
@@ -140,12 +157,19 @@ struct DevCtx {
         const uint32_t c = *nsl;
         if (c < a.cap) a.slots[((size_t)seg * a.cap + c) * a.nr + r] = idx;
         *nsl = c + 1u;
+        if (NIB) {  // A: listed; B: I_{i+1} <= prop_k (fthr = prop_k + prop_s + 1), a candidate that never settles
+            const uint32_t bit = 1u << (block & (GROUP - 1u));
+            cnt[K1_MA][r & 255u] |= bit;
+            if ((w1 >> 5) + a.ps < fthr) cnt[K1_MA + 1][r & 255u] |= bit;
+        }
     }
     __device__ __forceinline__ uint32_t run() const { return r0 + (tid & 63u); }
+    // NIB: records per super-group (msim_pipeline.h pipe_layout_nr)
     __device__ void group_start(uint32_t g, uint32_t w0, const Rng &ri, const Rng &rp)
     {
+        if (NIB && g % SGROUP) return;
         const uint32_t r = run();
-        const size_t gi = (size_t)jb * a.gps + g;
+        const size_t gi = NIB ? (size_t)jb * ((a.gps + SGROUP - 1) / SGROUP) + g / SGROUP : (size_t)jb * a.gps + g;
         GroupRec gr;
         gr.ri = ri;
         gr.rp = rp;
@@ -157,7 +181,7 @@ struct DevCtx {
     }
     __device__ void group(uint32_t g, uint32_t sum, uint64_t end)
     {
-        a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum;
+        if (!NIB) a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum;
         if (g % SGROUP == SGROUP - 1 || g + 1 == a.gps) {
             const uint32_t nsg = (a.gps + SGROUP - 1) / SGROUP;
             a.gend[((size_t)jb * nsg + g / SGROUP) * a.nr + run()] = end;
@@ -184,14 +208,14 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     __shared__ struct {
         PickTab pick;
         LogTab log;
-        uint32_t cnt[K1_OWNERS + 1][256];
+        uint32_t cnt[K1_ROWS][256];
     } sm;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < sizeof(PickTab) / 4; i += 256) ((uint32_t *)&sm.pick)[i] = ((const uint32_t *)a.tab.pick)[i];
     for (uint32_t i = tid; i < sizeof(LogTab) / 8; i += 256) ((double *)&sm.log)[i] = ((const double *)a.tab.logt)[i];
     auto s_cnt = sm.cnt;
 #pragma unroll
-    for (uint32_t w = 0; w <= K1_OWNERS; ++w) s_cnt[w][tid] = 0;
+    for (uint32_t w = 0; w < K1_ROWS; ++w) s_cnt[w][tid] = 0;
     __syncthreads();
 
     const uint32_t r = blockIdx.x * 256 + tid;  // slice-local run (< nr)

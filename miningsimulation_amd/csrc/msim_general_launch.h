@@ -46,11 +46,14 @@ struct GenTier {
 };
 
 // Window tiers for networks of up to max_m miners and runs of up to max_duration ms: 256 blocks (every
-// honest or minority-selfish run folds well inside it), 4 096, and the largest chain a run can have (a
-// selfish miner that never reveals: every block, mu + 10 sigma + 64). Lanes per tier fill `budget` bytes:
-// whole waves while a wave fits, down to ONE lane for a window too large for a wave (the last tier of a
-// large network: a run only reaches it with a selfish majority, and a lane serves its list in turn).
-constexpr double GEN_MAX_LANE_BYTES = 8.0 * 1024 * 1024 * 1024;  // one lane's chains: larger networks are rejected
+// honest or minority-selfish run folds well inside it), 4 096, and, for networks with a selfish miner, the
+// largest chain a run can have (a selfish miner that never reveals: every block, mu + 10 sigma + 64). Honest
+// networks stop at 4 096: their forks fold far inside it, and a run that outgrew it anyway would fail with
+// MSIM_E_CAPACITY rather than reserve a window it never uses. Lanes per tier fill `budget` bytes: whole waves
+// while a wave fits, down to ONE lane for a window too large for a wave (the last tier of a large selfish
+// network: a run only reaches it with a selfish majority, and a lane serves its list in turn).
+// One lane's chains may take up to a third of the MI355X's 288 GB of HBM; larger networks are rejected.
+constexpr double GEN_MAX_LANE_BYTES = 96.0 * 1024 * 1024 * 1024;
 inline double gen_lane_bytes(uint32_t max_m, uint32_t cap) { return (double)max_m * (cap * 12.0 + 12.0); }
 inline uint32_t gen_last_cap(int64_t max_duration)
 {
@@ -59,10 +62,10 @@ inline uint32_t gen_last_cap(int64_t max_duration)
     top = (top + 255) / 256 * 256;
     return (uint32_t)(top > 4096 ? top : 4096);
 }
-inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTier (&t)[3])
+inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTier (&t)[3], bool selfish)
 {
     const uint32_t caps[3] = {256u, 4096u, gen_last_cap(max_duration)};
-    const int nt = caps[2] > 4096u ? 3 : 2;
+    const int nt = selfish && caps[2] > 4096u ? 3 : 2;
     for (int i = 0; i < nt; ++i) {
         double l = floor(budget / gen_lane_bytes(max_m, caps[i]));
         l = l >= 64.0 ? floor(l / 64.0) * 64.0 : (l >= 1.0 ? l : 1.0);
@@ -73,7 +76,10 @@ inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTie
     return nt;
 }
 // Whether G can hold a network of m miners and runs of duration_ms (one lane of its last window).
-inline bool gen_fits(uint32_t m, int64_t duration_ms) { return gen_lane_bytes(m, gen_last_cap(duration_ms)) <= GEN_MAX_LANE_BYTES; }
+inline bool gen_fits(uint32_t m, int64_t duration_ms, bool selfish)
+{
+    return gen_lane_bytes(m, selfish ? gen_last_cap(duration_ms) : 4096u) <= GEN_MAX_LANE_BYTES;
+}
 
 // Workspace of G: the tier lists and the largest tier's chains and counters.
 struct GenWs {
@@ -83,11 +89,11 @@ struct GenWs {
     size_t lists_off, sizes_off, owners_off, arrivals_off, total;
 };
 
-inline GenWs gen_ws_layout(uint32_t max_m, int64_t max_duration, uint32_t list_cap, double budget)
+inline GenWs gen_ws_layout(uint32_t max_m, int64_t max_duration, uint32_t list_cap, double budget, bool selfish)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     GenWs w;
-    w.nt = gen_tiers(max_m, max_duration, budget, w.tier);
+    w.nt = gen_tiers(max_m, max_duration, budget, w.tier, selfish);
     w.list_cap = list_cap;
     size_t lanes = 0, chain = 0;
     for (int i = 0; i < w.nt; ++i) {

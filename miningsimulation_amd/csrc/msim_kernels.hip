@@ -173,8 +173,10 @@ __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int3
 #endif
 constexpr int K2_TPB = MSIM_K2_TPB, K3_TPB = MSIM_K3_TPB;
 static_assert(K3_TPB % 64 == 0 && K3_TPB <= TPB && TPB % K3_TPB == 0, "K3 workgroups: whole waves, dividing TPB");
-template <int M, bool LEAN>
-__global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_WAVES, 8))) void msim_episode_kernel(const SimParams p,
+// The mid and full state machines at two waves per SIMD (256 VGPRs): at three (168) the mid one spilled 31
+// VGPRs, the full one 132; a rho > 0.002 network lists ~10x the lean one's blocks, so K2 still fills the chip.
+template <int M, int KIND>
+__global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? MSIM_K2_WAVES : 2, 8))) void msim_episode_kernel(const SimParams p,
                                                                                                     const PipeArgs a)
 {
     // the draw tables in LDS: an episode's draws read them in its dependent chain (global: ~600-900 cycles
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(MSIM_K2_
     la.tab.pick = &s_pick;
     const uint32_t cnt = *a.list_count;
     const uint32_t lim = cnt < a.lcap ? cnt : a.lcap;
-    for (uint32_t idx = blockIdx.x * K2_TPB + threadIdx.x; idx < lim; idx += gridDim.x * K2_TPB) episode_entry<M, LEAN>(p, la, idx);
+    for (uint32_t idx = blockIdx.x * K2_TPB + threadIdx.x; idx < lim; idx += gridDim.x * K2_TPB) episode_entry<M, KIND>(p, la, idx);
 }
 
 // K3: one lane per run (msim_pipeline.h combine_run), then the MinerStats reduction.
@@ -303,6 +305,8 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.lcap = L.lcap;
     da.lchunk = L.lchunk;
     da.nib = nullptr;
+    da.cmask = nullptr;
+    da.ps = 0;
     da.segsum = (uint64_t *)(ws + L.segsum_off);
     da.segcnt = (uint32_t *)(ws + L.segcnt_off);
     da.nslow = (uint32_t *)(ws + L.nslow_off);
@@ -330,8 +334,9 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
         hipError_t e = launch_draws(da, a.stream);
         if (ee) (void)hipEventRecord(ee, a.stream);
         if (e != hipSuccess) return e;
-        if (L.k2_lean) hipLaunchKernelGGL((msim_episode_kernel<M, true>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
-        else hipLaunchKernelGGL((msim_episode_kernel<M, false>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
+        if (L.k2_kind == 0) hipLaunchKernelGGL((msim_episode_kernel<M, 0>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
+        else if (L.k2_kind == 1) hipLaunchKernelGGL((msim_episode_kernel<M, 1>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
+        else hipLaunchKernelGGL((msim_episode_kernel<M, 2>), dim3(ep_grid), dim3(K2_TPB), 0, a.stream, a.p, pa);
         hipLaunchKernelGGL((msim_combine_kernel<M>), dim3((cn + K3_TPB - 1) / K3_TPB), dim3(K3_TPB), 0, a.stream, a.p, pa,
                            cn, off, parts + (size_t)(off / K3_TPB) * 6 * M, a.records, a.best_h, a.err_count, a.err_list,
                            a.err_cap);

@@ -30,13 +30,19 @@
 
 namespace msim {
 
-// K2's state machine comes in two sizes. The lean one (networks with rho <= K2_LEAN_RHO) holds 2 extra
-// in-flight blocks and no deep-branch counters: an episode that needs more (a miner with 4 of its own blocks in
-// flight, or a fork deeper than the 16-height window) flags its run, which the retry kernel recomputes. At
-// rho <= 0.002 that is < 1e-3 of the runs of a 12-month simulation; configs[1] (rho = 1.7e-4): K2 125 -> 77 us
-// per launch (no spills instead of 134 VGPR spills; profiles/r04/k2v). Above it the full capacities (4 extra
-// blocks, deep branches) keep the retries rare.
+// K2's state machine comes in three sizes (KIND). Lean (0: networks with rho <= K2_LEAN_RHO): 2 extra in-flight
+// blocks and no deep-branch counters; at rho <= 0.002 an episode that needs more is < 1e-3 of the runs of a
+// 12-month simulation; configs[1] (rho = 1.7e-4): K2 125 -> 77 us per launch (no spills instead of 134 VGPR
+// spills; profiles/r04/k2v). Mid (1: every other pipeline network, rho <= PIPE_MAX_RHO): 4 extra blocks, no
+// deep branches — a fork deeper than the 16-height window needs 16 finds inside one propagation delay, which
+// no network the pipeline takes (delays up to ~50 s) makes in practice, and an episode that would is flagged
+// and its run recomputed by the retry kernel. Full (2): deep branches too (kept for A/B builds).
+// An episode that outgrows its capacities flags its run for the retry kernel: results never depend on them.
 constexpr double K2_LEAN_RHO = 0.002;
+#ifndef MSIM_K2_KIND_HI
+#define MSIM_K2_KIND_HI 1  // K2 above K2_LEAN_RHO: 1 mid, 2 full (A/B builds)
+#endif
+constexpr uint32_t K2_KIND_HI = MSIM_K2_KIND_HI;
 constexpr uint32_t GROUP = 32;          // blocks per group (end-of-run search metadata)
 constexpr uint32_t SGROUP = 8;          // groups per super-group (K3 searches super-group ends, then groups)
 constexpr uint32_t MIN_SEG = 512;       // shortest K1 worker (keeps the jump-ahead cost < 5 %)
@@ -55,6 +61,12 @@ struct EpEntry {
     uint32_t w0, w1;  // (interval << 5 | finder) of the block and of the next one
     uint32_t pad[2];
     Rng ri, rp;       // both streams, positioned at the block after w1
+};
+
+// The selfish pipeline's candidate masks of one 32-block chunk of a run (msim_selpipe.h): bit i of a = block
+// 32c + i is listed, of b = it is listed and I_{i+1} <= prop_k.
+struct alignas(8) CMask {
+    uint32_t a, b;
 };
 
 // A group of the band (where a run can end): the first block's word and both streams after it.
@@ -77,7 +89,7 @@ struct PipeLayout {
     uint32_t lcap;     // episode list capacity
     uint32_t lchunk;   // list slots a K1 wave reserves at a time (one atomic per chunk, not per append)
     uint32_t rec_words;
-    uint32_t k2_lean;  // K2 runs the lean state machine (rho <= K2_LEAN_RHO)
+    uint32_t k2_kind;  // K2's state machine: 0 lean (rho <= K2_LEAN_RHO), 1 mid, 2 full (msim_kernels.hip)
     size_t segsum_off, segcnt_off, nslow_off, slots_off, gsum_off, gend_off, gcum_off, grec_off, list_off, recs_off,
         count_off, total;
 };
@@ -105,7 +117,9 @@ struct DrawArgs {
     GroupRec *grec;       // [nband][gps][nr]
     EpEntry *list;        // [lcap]
     uint32_t *list_count;
-    uint32_t *nib;        // selfish pipeline only: [nb / 8][nr] finder nibbles, block 8w + i in bits 4i..4i+3
+    uint32_t *nib;        // selfish pipeline only: finder nibbles, 16-byte chunks of 32 blocks (msim_selpipe.h)
+    CMask *cmask;         // selfish pipeline only: [nb / 32][nr] candidate masks (msim_selpipe.h SpArgs)
+    uint32_t ps;          // selfish pipeline only: the selfish miner's delay
 };
 
 struct PipeArgs {  // K2 / K3
@@ -132,25 +146,19 @@ enum : uint32_t { REC_ENDED = 1u, REC_ERR = 2u, REC_SKIP = 4u };
 // `slots` = wave slots of K1 on the device (CUs x resident waves per CU). The run is cut into `nseg`
 // workers of `seg` blocks so that the K1 grid fills the device in whole rounds: every wave does the
 // same work, so a partial last round would leave SIMDs idle.
-inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget,
-                                  uint32_t slots)
+// The layout of a slice of exactly nr runs (a multiple of 256). recs: the honest pipeline (K2's episode
+// records; band records per group). !recs: the selfish pipeline, which reads the list entries themselves and
+// keeps band records (counts and RNG states) per super-group only, and no group sums (msim_selpipe.h sp_begin).
+inline PipeLayout pipe_layout_nr(double rho, uint32_t m, int64_t duration_ms, uint32_t nr, uint32_t slots, bool recs)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     PipeLayout L;
     const double D = (double)duration_ms;
     const double mu = D / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
     const double need = mu + 8.0 * sd + 64.0;  // blocks to pre-generate (P(more) < 1e-15 per run)
-    const uint64_t want = (n_runs + 255) / 256 * 256;
-    // slice size first (memory), with an upper estimate of the per-run bytes
-    L.rec_words = 3 + 2 * m;
-    L.k2_lean = rho <= K2_LEAN_RHO ? 1u : 0u;
-    const double nb_est = need + 2.0 * MIN_SEG;
-    const double per_run = 64.0 * (8.0 + CNT_WORDS * 4 + 4) + 4.0 * (rho * nb_est * 2 + 64.0 * 16) +
-                           2.0 * nb_est / GROUP * (4.0 + 8.0 / SGROUP + CNT_WORDS * 4 + sizeof(GroupRec)) +
-                           rho * nb_est * (sizeof(EpEntry) + 4.0 * L.rec_words);
-    uint64_t cap_runs = (uint64_t)(budget / per_run) / 256 * 256;
-    if (cap_runs < 256) cap_runs = 256;
-    L.nr = (uint32_t)(want < cap_runs ? want : cap_runs);
+    L.rec_words = recs ? 3 + 2 * m : 0;
+    L.k2_kind = rho <= K2_LEAN_RHO ? 0u : K2_KIND_HI;
+    L.nr = nr;
     // workers per run: minimise rounds(w) * (seg(w) + jump cost), jump ~ 25 blocks of work
     const double rows = L.nr / 64.0;
     if (slots < 1) slots = 1;
@@ -180,7 +188,7 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     L.cap = (uint32_t)ceil(lam + 8.0 * sqrt(lam) + 8.0);
     const double ent = (double)L.nr * rho * L.nb;
     // A K1 wave reserves list slots a chunk at a time: one same-address atomic per chunk instead of one per
-    // append (at rho = 1.7 % — configs[0] — the per-append atomics serialised K1 to 56x its draw time). The
+    // append (at rho = 1.7 % — configs[0] — the per-append atomics serialised K1 to 30x its draw time). The
     // chunk follows a wave's expected appends; its unused tail (< lchunk slots per wave) is marked EP_HOLE.
     const double per_wave = 64.0 * rho * L.seg;
     L.lchunk = 16;
@@ -196,14 +204,15 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     o = al(o + (size_t)L.nseg * L.nr * 4);
     L.slots_off = o;
     o = al(o + (size_t)L.nseg * L.cap * L.nr * 4);
+    const size_t grp = recs ? L.gps : L.nsg;  // band records per segment
     L.gsum_off = o;
-    o = al(o + (size_t)L.nband * L.gps * L.nr * 4);
+    o = al(o + (recs ? (size_t)L.nband * L.gps * L.nr * 4 : 0));
     L.gend_off = o;
     o = al(o + (size_t)L.nband * L.nsg * L.nr * 8);
     L.gcum_off = o;
-    o = al(o + (size_t)L.nband * L.gps * CNT_WORDS * L.nr * 4);
+    o = al(o + (size_t)L.nband * grp * CNT_WORDS * L.nr * 4);
     L.grec_off = o;
-    o = al(o + (size_t)L.nband * L.gps * L.nr * sizeof(GroupRec));
+    o = al(o + (size_t)L.nband * grp * L.nr * sizeof(GroupRec));
     L.list_off = o;
     o = al(o + (size_t)L.lcap * sizeof(EpEntry));
     L.recs_off = o;
@@ -212,6 +221,21 @@ inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, u
     o = al(o + 4);
     L.total = o;
     return L;
+}
+
+// The largest slice (all n_runs, or fewer) whose layout, plus extra_per_run bytes per run, fits the budget.
+inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget,
+                                  uint32_t slots, bool recs = true, double extra_per_run = 0.0)
+{
+    uint64_t nr = (n_runs + 255) / 256 * 256;
+    for (;;) {
+        const PipeLayout L = pipe_layout_nr(rho, m, duration_ms, (uint32_t)nr, slots, recs);
+        const double tot = (double)L.total + extra_per_run * (double)nr;
+        if (tot <= budget || nr <= 256) return L;
+        uint64_t next = (uint64_t)((double)nr * budget / tot * 0.98) / 256 * 256;
+        if (next >= nr) next = nr - 256;
+        nr = next < 256 ? 256 : next;
+    }
 }
 
 // ---------------------------------------------------------------- K1 lane body (shared host/device)
@@ -292,10 +316,10 @@ MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, cons
 // One (run, segment) worker: SEG blocks from the jumped RNG states. Ctx supplies the side effects:
 //   count(info)                       per-owner counter of this lane (+1 for owner info_finder(info))
 //   vote(s)                           nonzero when s holds for some active lane of the wave (host: s)
-//   slow(s, block, offset, w0, w1, ri, rp)
+//   slow(s, block, offset, w0, w1, ri, rp, fthr)
 //                                     called after a nonzero vote: records a non-fast block when s
 //                                     (offset = its find time minus the segment's start; its word, the
-//                                     next one and both streams after them)
+//                                     next one and both streams after them; the finder's threshold)
 //   group(g, sum, end)                band only: sum of the group's intervals, and the time from the segment's
 //                                     start to the group's end
 //   quad()                            start of a quad of blocks
@@ -358,7 +382,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
                         rng_next(b);
                     }
                     cx.slow(slow, b0 + g * GROUP + q4 * K1_QB + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
-                            (I[q] << 5) | info_finder(info[q]), a, b);
+                            (I[q] << 5) | info_finder(info[q]), a, b, info_fthr(infocur));
                 }
                 Icur = I[q];
                 infocur = info[q];
@@ -419,6 +443,9 @@ MSIM_HD uint32_t add_packed(uint32_t (&F)[M], const uint32_t *__restrict__ src, 
 #define MSIM_K3_EP_MAX 32  // 24: 76.8 us, 16: 99.1 us vs 67.7 us per c2 launch (more runs on the one-read-at-a-time path)
 #endif
 constexpr uint32_t K3_SEG_MAX = 32, K3_EP_MAX = MSIM_K3_EP_MAX, K3_SCRATCH = K3_SEG_MAX + 2 * K3_EP_MAX;
+// combine_run keeps its candidate starts in the segment-count rows (nsw[na * nss], na < K3_EP_MAX): a larger
+// K3_EP_MAX would overwrite the record indices at rows K3_SEG_MAX + t before they are read
+static_assert(K3_EP_MAX <= K3_SEG_MAX, "MSIM_K3_EP_MAX must not exceed K3_SEG_MAX");
 template <int M>
 MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint32_t (&F)[M], uint32_t (&S)[M],
                          uint32_t *nsw, size_t nss)
@@ -755,7 +782,7 @@ MSIM_HD bool combine_run(const SimParams &p, const PipeArgs &a, uint32_t r, uint
 }
 
 // ---------------------------------------------------------------- K2 lane body (shared host/device)
-template <int M, bool LEAN>
+template <int M, int KIND>
 MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
 {
     const EpEntry e = a.list[idx];
@@ -787,7 +814,7 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     src.nxt = e.w1;
     src.have_nxt = true;
     // K2's capacities (K2_LEAN_RHO above); the retry kernel recomputes a flagged run with NX_WIDE and deep branches
-    Sim<M, false, !LEAN, LEAN ? 2 : NX_FAST, NG_FAST> s;
+    Sim<M, false, KIND == 2, KIND == 0 ? 2 : NX_FAST, NG_FAST> s;
     EpisodeOut<M> o;
     s.episode(p, src, T, o);
     rec[0] = o.end;

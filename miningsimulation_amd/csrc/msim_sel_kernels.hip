@@ -198,6 +198,9 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #ifndef SEL_ENGPROF
 #define SEL_ENGPROF 0
 #endif
+#ifndef SP_PROF
+#define SP_PROF 0
+#endif
 #ifndef SEL_MSTEPS
 #define SEL_MSTEPS 2
 #endif
@@ -458,6 +461,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 #endif
 }
 
+// The selfish pipeline's engine source takes back K1's count of every block below B the engine consumes.
+template <int M>
+struct SpCntDev {
+    uint32_t *c;  // &s_cnt[0][tid]
+    __device__ __forceinline__ void add(uint32_t k, uint32_t v) { atomicAdd(&c[(C_F * M + (int)k) * TPB], v); }
+};
+
 // S2 of the selfish pipeline (msim_selpipe.h): one lane per run of the slice, one network (point 0). The
 // lane applies the settled-state transition from K1's finder nibbles (the nibble phase, all lanes a word at
 // a time) until a candidate needs the engine or the run reaches B; such lanes wait, and when xth of them wait
@@ -471,7 +481,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
     __shared__ uint32_t s_mc[SelMacro<M>::NW][TPB];
-    __shared__ uint32_t s_cur[SpCur::NW][TPB];
+    __shared__ uint32_t s_cur[SpCur::NW + 1][TPB];  // the cursor, and the block the engine hands back
     __shared__ int64_t s_prop[MAXM];
     __shared__ uint8_t s_lut[128];
     __shared__ LogTab s_log[1];
@@ -537,18 +547,31 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         err |= r.err;
     };
     auto vote = [](bool b) { return __builtin_amdgcn_ballot_w64(b) != 0ull; };
+#if SP_PROF  // per-wave phase timing (diagnostic builds only: scripts/build_variant.sh ... -DSP_PROF=1)
+    uint64_t pt_n = 0, pt_e = 0, pn_n = 0, pn_e = 0, pi_n = 0, pi_e = 0, pl_n = 0, pl_e = 0;
+    const uint64_t pt0 = clock64();
+#endif
     for (;;) {
         const uint64_t bn = __builtin_amdgcn_ballot_w64(mode == 0);
         const uint64_t bw = __builtin_amdgcn_ballot_w64((mode == 1) | (mode == 4));
         if ((bn | bw) == 0ull) break;
+#if SP_PROF
+        const uint64_t pc0 = clock64();
+        const bool peng = bw != 0ull && (__builtin_popcountll(bw) >= xth || bn == 0ull);
+#endif
+#if SP_DIAG_NOENG  // diagnostic builds only: the nibble phase without the engine's code (wrong results)
+        if (bw != 0ull) {
+            mode = ((mode == 1) | (mode == 4)) ? 3 : mode;
+        } else
+#endif
         if (bw != 0ull && (__builtin_popcountll(bw) >= xth || bn == 0ull)) {
             mc.save(mcs, TPB);
             cur.save(cs, TPB);
             Sel<M, 1, 1, 4, 1, SEL_NC> s;
-            SpSrc<SelFifo<SelFastDraw<M>>, SelDevEnv<M, UNI>> src;
+            SpSrc<SelFifo<SelFastDraw<M>>, SpCntDev<M>> src;
             src.f.d = drawer();
             src.f.n = 0;
-            src.env = env;
+            src.cnt.c = &s_cnt[0][tid];
             src.pidx = SP_NONE;
             src.pk = 0;
             src.B = cur.B;
@@ -568,24 +591,30 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
                         SelMacro<M> tb;
                         if (tb.take_back(env, s, sid)) {  // back to the nibble form at src.pidx (sp_seek below)
                             tb.save(mcs, TPB);
-                            cs[0] = src.pidx;  // SpCur::pos
+                            cs[SpCur::NW * TPB] = src.pidx;
                             mode = 7;
                         }
                     }
                 }
+#if SP_PROF
+                ++pi_e;
+                pl_e += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 2));
+#endif
                 if (__builtin_amdgcn_ballot_w64(mode == 2) == 0ull) break;
             }
             mc.load(mcs, TPB);
             cur.load(cs, TPB);
-            if (mode == 7) {
-                sp_seek(sa, lr, cur, cur.pos);
+            if (mode == 7) {  // handed back by the engine: resume at its pending block
+                sp_seek(sa, lr, cur, cs[SpCur::NW * TPB]);
                 mode = cur.err ? 3 : 0;
                 err |= cur.err;
+            } else if (mode == 0) {  // waited in the nibble form: its chunks were not kept through the phase
+                sp_refill(sa, lr, cur);
             }
         } else {
             for (;;) {
                 if (mode == 0) {
-                    mode = sp_word<M>(sa, lr, env, vote, cur, mc, sid, D);
+                    mode = sp_chunk<M>(sa, lr, env, vote, cur, mc, sid, D);
                     if (mode == 6) {
                         SelOut r;
                         mc.finish(env, sid, r);
@@ -594,12 +623,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
                     }
                     if (mode == 3) err |= cur.err;
                 }
+#if SP_PROF
+                ++pi_n;
+                pl_n += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 0));
+#endif
                 if (__builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
                     __builtin_popcountll(__builtin_amdgcn_ballot_w64((mode == 1) | (mode == 4))) >= xth)
                     break;
             }
         }
+#if SP_PROF
+        const uint64_t pc1 = clock64();
+        if (peng) {
+            pt_e += pc1 - pc0;
+            ++pn_e;
+        } else {
+            pt_n += pc1 - pc0;
+            ++pn_n;
+        }
+#endif
     }
+#if SP_PROF
+    if (blockIdx.x < 2 && (threadIdx.x & 63u) == 0u)
+        printf("SPPROF blk %u wave %u total %llu | nibble phases %llu cyc %llu words %llu lanes %llu | engine phases %llu cyc %llu iters %llu lanes %llu\n",
+               blockIdx.x, threadIdx.x / 64u, (unsigned long long)(clock64() - pt0), (unsigned long long)pn_n,
+               (unsigned long long)pt_n, (unsigned long long)pi_n, (unsigned long long)pl_n, (unsigned long long)pn_e,
+               (unsigned long long)pt_e, (unsigned long long)pi_e, (unsigned long long)pl_e);
+#endif
     SelOut o;
     o.err = err;
     o.best_height = bh;

@@ -9,15 +9,19 @@
 //
 //   K1<NIB>  msim_draws_kernel (msim_drawgen.hip, the honest pipeline's draw kernel, msim_pipeline.h):
 //            (run, segment) workers jumped to their segment, every block drawn as the reference draws it
-//            (simulation.h:205-221); per block it stores the finder as a 4-bit nibble ([nb/8][nr] words)
+//            (simulation.h:205-221); per block it stores the finder as a 4-bit nibble (a 16-byte chunk of 32
+//            blocks per run, [nb/32][nr] chunks, so S2 reads a run's chunk with one 16-byte load)
 //            and counts it per owner; it lists a block (with both RNG states after the next block) when
 //            its finder is honest and the next interval is <= prop_k + prop_s: only such a "candidate"
 //            can need the engine (msim_selm.h step: an honest find settles iff I_next > prop_k, or
 //            > prop_k + prop_s when the selfish miner withholds blocks). Selfish finds are never listed.
+//            Per 32-block chunk it also writes two candidate masks: A (the block is listed) and B (its
+//            I_next <= prop_k: it never settles), so S2 decides every candidate from its chunk alone.
 //   S2       msim_selpipe_kernel (msim_sel_kernels.hip): one lane per run, the settled-state transition
-//            for every block from its nibble alone (no draw, no counter: ~40 instructions per block), the
-//            candidates checked against the state, and the engine for those that need it, drawing its
-//            episode from the candidate's stored RNG states. The block where the nibble form stops, B (the
+//            for every block from its nibble and mask bits alone (no draw, no counter, no memory access but
+//            one 16-byte chunk and one mask pair per 32 blocks, loaded a chunk ahead), and the engine for
+//            the candidates that need it, drawing the episode from the candidate's stored RNG states (found
+//            through the run's slot list only then). The block where the nibble form stops, B (the
 //            first block with T_B >= D - max(prop_k + prop_s)), is found in the prologue from K1's band sums
 //            and one group redrawn from its stored RNG states; the run then ends right after B - 1 (T_B >= D,
 //            ~99.7 % of runs at 1 s) or the engine finishes it from B with draws from the same group record,
@@ -61,18 +65,19 @@ inline double sp_rho(const uint64_t *perc, const int64_t *prop, const uint8_t *s
 // The honest pipeline's layout (msim_pipeline.h) sized for the candidate rate, plus the nibbles.
 struct SpLayout {
     PipeLayout L;
-    size_t nib_off, total;
+    size_t nib_off, cmask_off, total;
 };
 inline SpLayout sp_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget,
                               uint32_t slots)
 {
     SpLayout s;
-    s.L = pipe_layout_for(rho, m, duration_ms, n_runs, budget, slots);
-    const double nib = (double)s.L.nr * s.L.nb / 2.0;
-    if ((double)s.L.total + nib > budget)  // shrink the slice so that both fit
-        s.L = pipe_layout_for(rho, m, duration_ms, n_runs, budget * (double)s.L.total / ((double)s.L.total + nib), slots);
+    const double mu = (double)duration_ms / 599999.5;
+    // >= nb / 2 bytes of nibbles and nb / 4 bytes of candidate masks per run
+    const double nib = (mu + 8.0 * sqrt(mu > 1.0 ? mu : 1.0) + 64.0 + GROUP * 256.0) * 0.75;
+    s.L = pipe_layout_for(rho, m, duration_ms, n_runs, budget, slots, false, nib);
     s.nib_off = (s.L.total + 255) / 256 * 256;
-    s.total = s.nib_off + ((size_t)s.L.nb / 8 * s.L.nr * 4 + 255) / 256 * 256;
+    s.cmask_off = s.nib_off + ((size_t)s.L.nb / 8 * s.L.nr * 4 + 255) / 256 * 256;
+    s.total = s.cmask_off + ((size_t)s.L.nb / 32 * s.L.nr * 8 + 255) / 256 * 256;
     return s;
 }
 
@@ -105,36 +110,39 @@ inline void build_pick_table_sp(const uint64_t *perc, const int64_t *prop, const
 
 // What S2 reads of K1's output (one slice).
 struct SpArgs {
-    uint32_t nr, seg, gps, nsg, nseg, nb, cap, band_lo, lcap;
+    uint32_t nr, seg, nsg, nseg, nb, cap, band_lo, lcap;
     const uint64_t *segsum;  // [nseg][nr]
     const uint32_t *segcnt;  // [nseg][8][nr] packed u16 owner counts
     const uint32_t *nslow;   // [nseg][nr] candidates per segment
     const uint32_t *slots;   // [nseg][cap][nr] list indices, block order
-    const uint32_t *gsum;    // [nband][gps][nr]
-    const uint64_t *gend;    // [nband][nsg][nr]
-    const uint32_t *gcum;    // [nband][gps][8][nr]
-    const GroupRec *grec;    // [nband][gps][nr]
+    const uint64_t *gend;    // [nband][nsg][nr]: time from the segment's start to each super-group's end
+    const uint32_t *gcum;    // [nband][nsg][8][nr]: counts before each super-group
+    const GroupRec *grec;    // [nband][nsg][nr]: each super-group's first block and the streams after it
     const EpEntry *list;
-    const uint32_t *nib;     // [nb/8][nr]
+    const uint32_t *nib;     // [nb/32][nr][4]: word w (blocks 8w .. 8w+7) of run r at ((w >> 2) * nr + r) * 4 + (w & 3)
+    const CMask *cmask;      // [nb/32][nr]: per chunk (A: listed candidates, B: candidates with I_next <= prop_k)
 };
 
-// The nibble-mode cursor of one run (saved to LDS around engine phases on the device).
+// The u32 index of nibble word w of run r (the 16-byte chunk layout above; K1 writes it, S2 reads it).
+MSIM_HD size_t sp_nib_index(uint32_t nr, uint32_t r, uint32_t w) { return ((size_t)(w >> 2) * nr + r) * 4 + (w & 3u); }
+
+// The nibble-form cursor of one run (saved to LDS around engine phases on the device).
 struct SpCur {
     uint32_t pos;          // pending block (the next find the settled form applies)
     uint32_t B;            // the first block with T_B >= D - max(prop_k + prop_s): the nibble form stops there
-    uint32_t cseg, ci, cn; // candidate cursor: segment, next slot, candidates of that segment
-    uint32_t c0, w0, i0;   // next candidate: block, next block's word (I << 5 | k), list index
-    uint32_t c1, w1, i1;   // the one after it (prefetched)
     uint32_t sg;           // segment of pos
+    uint32_t ci;           // candidates of segment sg below pos (the slot of the next one)
     uint64_t Tseg;         // time of the last block before segment sg (sum of the segment sums below it)
     uint64_t TB;           // T_B
-    uint32_t gE;           // band position of B's group: jb * gps + g
+    uint32_t gE;           // band position of B's super-group: jb * nsg + q
     uint32_t err;
-    static constexpr int NW = 18;
+    uint32_t A[4], N[4];   // the nibble chunk of pos (blocks 32c .. 32c + 31) and the next one, loaded ahead
+    CMask mA, mN;          // their candidate masks (not saved with the cursor: reloaded, sp_refill)
+    static constexpr int NW = 10;
     MSIM_HD void save(uint32_t *p, int st) const
     {
-        const uint32_t v[NW] = {pos, B, cseg, ci, cn, c0, w0, i0, c1, w1, i1, sg, (uint32_t)Tseg, (uint32_t)(Tseg >> 32),
-                                (uint32_t)TB, (uint32_t)(TB >> 32), gE, err};
+        const uint32_t v[NW] = {pos, B, sg, ci, (uint32_t)Tseg, (uint32_t)(Tseg >> 32), (uint32_t)TB, (uint32_t)(TB >> 32),
+                                gE, err};
 #pragma unroll
         for (int i = 0; i < NW; ++i) p[i * st] = v[i];
     }
@@ -142,83 +150,100 @@ struct SpCur {
     {
         pos = p[0];
         B = p[st];
-        cseg = p[2 * st];
+        sg = p[2 * st];
         ci = p[3 * st];
-        cn = p[4 * st];
-        c0 = p[5 * st];
-        w0 = p[6 * st];
-        i0 = p[7 * st];
-        c1 = p[8 * st];
-        w1 = p[9 * st];
-        i1 = p[10 * st];
-        sg = p[11 * st];
-        Tseg = (uint64_t)p[12 * st] | ((uint64_t)p[13 * st] << 32);
-        TB = (uint64_t)p[14 * st] | ((uint64_t)p[15 * st] << 32);
-        gE = p[16 * st];
-        err = p[17 * st];
+        Tseg = (uint64_t)p[4 * st] | ((uint64_t)p[5 * st] << 32);
+        TB = (uint64_t)p[6 * st] | ((uint64_t)p[7 * st] << 32);
+        gE = p[8 * st];
+        err = p[9 * st];
     }
 };
 
-// Next candidate of run r after the cursor (block SP_NONE when the run has no more).
-MSIM_HD void sp_fetch(const SpArgs &a, uint32_t r, SpCur &c, uint32_t &blk, uint32_t &wn, uint32_t &idx)
+// Nibble chunk c (blocks 32c .. 32c + 31) of run r and its candidate masks (one 16-byte and one 8-byte load);
+// beyond the pre-generated blocks, the last chunk.
+MSIM_HD void sp_chunk_at(const SpArgs &a, uint32_t r, uint32_t c, uint32_t (&w)[4], CMask &m)
 {
-    while (c.ci >= c.cn) {
-        if (++c.cseg >= a.nseg) {
-            blk = SP_NONE;
-            wn = 0;
-            idx = SP_NONE;
-            return;
-        }
-        c.cn = a.nslow[(size_t)c.cseg * a.nr + r];
-        c.ci = 0;
-        if (c.cn > a.cap) c.err |= SERR_SP;
-    }
-    idx = a.slots[((size_t)c.cseg * a.cap + c.ci) * a.nr + r];
-    c.ci++;
-    if (idx >= a.lcap || c.err) {
-        c.err |= SERR_SP;
-        blk = SP_NONE;
-        wn = 0;
-        return;
-    }
-    blk = a.list[idx].block;
-    wn = a.list[idx].w1;
+    const uint32_t last = a.nb / 32 - 1;
+    c = c < last ? c : last;
+    const uint32_t *q = a.nib + sp_nib_index(a.nr, r, c * 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint4 v = *(const uint4 *)q;  // one global_load_dwordx4
+    w[0] = v.x;
+    w[1] = v.y;
+    w[2] = v.z;
+    w[3] = v.w;
+#else
+    for (int i = 0; i < 4; ++i) w[i] = q[i];
+#endif
+    m = a.cmask[(size_t)c * a.nr + r];
 }
 
-// Drop the next candidate (consumed), pull the prefetched one forward.
-MSIM_HD void sp_pop(const SpArgs &a, uint32_t r, SpCur &c)
+// The finder nibble of block b of run r.
+MSIM_HD uint32_t sp_nib(const SpArgs &a, uint32_t r, uint32_t b)
 {
-    c.c0 = c.c1;
-    c.w0 = c.w1;
-    c.i0 = c.i1;
-    sp_fetch(a, r, c, c.c1, c.w1, c.i1);
+    return (a.nib[sp_nib_index(a.nr, r, b >> 3)] >> (4 * (b & 7u))) & 15u;
 }
 
-// Resume the nibble form at block pos: the candidates below it were consumed by the engine, and the
-// segment time follows pos.
+// Load the chunk of pos and the next one (the nibble form reads a chunk per 32 blocks with the next one in
+// flight, so its latency is hidden).
+MSIM_HD void sp_refill(const SpArgs &a, uint32_t r, SpCur &c)
+{
+    sp_chunk_at(a, r, c.pos >> 5, c.A, c.mA);
+    sp_chunk_at(a, r, (c.pos >> 5) + 1, c.N, c.mN);
+}
+
+// Candidates of run r among blocks [b0, b1) (their A mask bits; the chunks loaded here: rare paths only).
+MSIM_HD uint32_t sp_count_cands(const SpArgs &a, uint32_t r, uint32_t b0, uint32_t b1)
+{
+    uint32_t n = 0;
+    for (uint32_t c = b0 >> 5; c * 32 < b1; ++c) {
+        uint32_t m = a.cmask[(size_t)c * a.nr + r].a;
+        const uint32_t lo = b0 > c * 32 ? b0 - c * 32 : 0u, hi = b1 < c * 32 + 32 ? b1 - c * 32 : 32u;
+        m &= (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+        n += (uint32_t)__builtin_popcount(m);
+    }
+    return n;
+}
+
+// Resume the nibble form at block pos (after an engine episode that consumed blocks from cur.pos on): the
+// segment time and the candidate count follow pos.
 MSIM_HD void sp_seek(const SpArgs &a, uint32_t r, SpCur &c, uint32_t pos)
 {
-    c.pos = pos;
-    while (c.c0 != SP_NONE && c.c0 < pos) sp_pop(a, r, c);
+    uint32_t from = c.pos;
     while (pos >= (c.sg + 1) * a.seg) {
         c.Tseg += a.segsum[(size_t)c.sg * a.nr + r];
         c.sg++;
+        c.ci = 0;
+        from = c.sg * a.seg;
     }
+    c.ci += sp_count_cands(a, r, from, pos);
+    c.pos = pos;
+    sp_refill(a, r, c);
+}
+
+// First block of band super-group gE.
+MSIM_HD uint32_t sp_sg_block(const SpArgs &a, uint32_t gE)
+{
+    return (a.band_lo + gE / a.nsg) * a.seg + (gE % a.nsg) * (SGROUP * GROUP);
 }
 
 // Prologue of run r: B, the first block with T_B >= D - thr (thr = max over honest k of prop_k + prop_s), and
-// T_B — from K1's band sums (super-group ends, then group sums) and B's group redrawn from its record (the
-// group's first block word and both RNG states after it; drw: the lane's exact drawer, msim_selm.h) — and the
-// first two candidates.
+// T_B — from K1's super-group ends and B's super-group redrawn from its record (its first block's word and
+// both RNG states after it; drw: the lane's exact drawer, msim_selm.h; at most SGROUP * GROUP draws, once per
+// run) — and the first chunks. A run whose candidates outgrew a segment's slots is flagged (E2 recomputes it).
 template <class Drw>
 MSIM_HD void sp_begin(const SpArgs &a, uint32_t r, int64_t D, int64_t thr, Drw &drw, SpCur &c)
 {
     c.err = 0;
     c.pos = 0;
     c.sg = 0;
+    c.ci = 0;
     c.Tseg = 0;
     uint64_t Tb = 0;  // time of the last block before the band
-    for (uint32_t s = 0; s < a.band_lo; ++s) Tb += a.segsum[(size_t)s * a.nr + r];
+    for (uint32_t s = 0; s < a.nseg; ++s) {
+        if (s < a.band_lo) Tb += a.segsum[(size_t)s * a.nr + r];
+        if (a.nslow[(size_t)s * a.nr + r] > a.cap) c.err |= SERR_SP;
+    }
     const int64_t Dth = D - thr;
     c.B = SP_NONE;
     c.TB = 0;
@@ -236,75 +261,58 @@ MSIM_HD void sp_begin(const SpArgs &a, uint32_t r, int64_t D, int64_t thr, Drw &
             Tj += a.segsum[(size_t)(a.band_lo + jb) * a.nr + r];
             continue;
         }
-        uint64_t t = Tj + (sg ? a.gend[((size_t)jb * a.nsg + sg - 1) * a.nr + r] : 0ull);
-        const uint32_t g0 = sg * SGROUP, g1 = g0 + SGROUP < a.gps ? g0 + SGROUP : a.gps;
-        for (uint32_t g = g0; g < g1; ++g) {
-            const uint32_t gs = a.gsum[((size_t)jb * a.gps + g) * a.nr + r];
-            if ((int64_t)(t + gs) >= Dth) {
-                // B is in group g: redraw it from its first block (T_{W-1} = t)
-                const GroupRec gr = a.grec[((size_t)jb * a.gps + g) * a.nr + r];
-                drw.ri = gr.ri;
-                drw.rp = gr.rp;
-                uint32_t b = (a.band_lo + jb) * a.seg + g * GROUP;
-                uint64_t T = t + (gr.w0 >> 5);
-                for (uint32_t i = 1; i < GROUP && (int64_t)T < Dth; ++i) {
-                    uint32_t I, k;
-                    drw.draw(I, k);
-                    T += I;
-                    ++b;
-                }
-                c.B = b;
-                c.TB = T;
-                c.gE = jb * a.gps + g;
-                break;
-            }
-            t += gs;
+        // B is in super-group sg: redraw it from its first block (T of the block before it = t)
+        const uint64_t t = Tj + (sg ? a.gend[((size_t)jb * a.nsg + sg - 1) * a.nr + r] : 0ull);
+        c.gE = jb * a.nsg + sg;
+        const GroupRec gr = a.grec[(size_t)c.gE * a.nr + r];
+        drw.ri = gr.ri;
+        drw.rp = gr.rp;
+        uint32_t b = sp_sg_block(a, c.gE);
+        uint64_t T = t + (gr.w0 >> 5);
+        for (uint32_t i = 1; i < SGROUP * GROUP && (int64_t)T < Dth; ++i) {
+            uint32_t I, k;
+            drw.draw(I, k);
+            T += I;
+            ++b;
         }
+        c.B = b;
+        c.TB = T;
         break;
     }
     if (c.B == SP_NONE) c.err |= SERR_SP;  // the run outlasts the pre-generated blocks
-    c.cseg = 0;
-    c.ci = 0;
-    c.cn = a.nslow[r];
-    if (c.cn > a.cap) c.err |= SERR_SP;
-    sp_fetch(a, r, c, c.c0, c.w0, c.i0);
-    sp_fetch(a, r, c, c.c1, c.w1, c.i1);
+    sp_refill(a, r, c);
 }
 
 // K1's per-owner counts of blocks [0, B): the segments below B's segment, the cumulative counts at the start of
-// B's group (gcum), and the group's blocks before B (their finders from the nibbles).
+// B's super-group (gcum), and the super-group's blocks before B (their finders from the nibbles).
 template <int M>
 MSIM_HD void sp_counts(const SpArgs &a, uint32_t r, const SpCur &c, uint32_t (&F)[M])
 {
 #pragma unroll
     for (int k = 0; k < M; ++k) F[k] = 0;
-    const uint32_t jb = c.gE / a.gps;
+    const uint32_t jb = c.gE / a.nsg;
     for (uint32_t s = 0; s < a.band_lo + jb; ++s) add_packed<M>(F, a.segcnt + (size_t)s * CNT_WORDS * a.nr + r, a.nr);
     add_packed<M>(F, a.gcum + (size_t)c.gE * CNT_WORDS * a.nr + r, a.nr);
-    for (uint32_t b = c.B & ~(GROUP - 1u); b < c.B; ++b) {
-        const uint32_t k = (a.nib[(size_t)(b >> 3) * a.nr + r] >> (4 * (b & 7u))) & 15u;
+    for (uint32_t b = sp_sg_block(a, c.gE); b < c.B; ++b) {
+        const uint32_t k = sp_nib(a, r, b);
 #pragma unroll
         for (int kk = 0; kk < M; ++kk) F[kk] += (uint32_t)kk == k ? 1u : 0u;
     }
 }
 
-// One nibble word of a lane in the nibble form: the settled-state transition of every block from
-// max(pos, the word's first block) up to the word's end or B, from the block's finder alone. A candidate is
-// checked against the state (msim_selm.h step: an honest find settles iff I_next > prop_k + (w ? prop_s : 0);
-// candidates have I_next <= prop_k + prop_s, so with w != 0 they never settle). Returns the lane's mode:
-// 0 (continue at the next word), 1 (cur.pos is a candidate that needs the engine), 4 (cur.pos == B: switch
-// to the engine: T_B < D), 6 (the run ends after block B - 1: T_B >= D, finish the settled form), 3 (error
-// in cur.err). vote(b): nonzero when b holds for some lane of the wave (host: b).
-template <int M, class Env, class Vote>
-MSIM_HD int sp_word(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur, SelMacro<M> &mc, uint32_t sid,
-                    int64_t D)
+// One nibble word (blocks 8 wi .. 8 wi + 7) of a lane in the nibble form: the settled-state transition of every
+// block from max(pos, 8 wi) up to the word's end or B, from the block's finder and candidate bits alone
+// (mA, mB: the word's bits of the chunk masks; a block whose finder fell through PickFinder is left to the
+// error check). A candidate settles (msim_selm.h step: an honest find settles
+// iff I_next > prop_k + (w ? prop_s : 0); a candidate has I_next <= prop_k + prop_s) iff its B bit is clear
+// and w == 0. Returns the lane's mode: 0 (continue), 1 (cur.pos is a candidate that needs the engine), 4
+// (cur.pos == B: to the engine, T_B < D), 6 (the run ends after block B - 1: T_B >= D, finish the settled
+// form), 3 (error in cur.err). vote(b): nonzero when b holds for some lane of the wave (host: b).
+template <int M, class Vote>
+MSIM_HD int sp_word(Vote vote, SpCur &cur, SelMacro<M> &mc, uint32_t sid, int64_t D, uint32_t word,
+                    uint32_t mA, uint32_t mB, uint32_t wi)
 {
-    if (cur.pos >= (cur.sg + 1) * a.seg) {  // segments start at word boundaries (seg is a multiple of GROUP)
-        cur.Tseg += a.segsum[(size_t)cur.sg * a.nr + r];
-        cur.sg++;
-    }
-    const uint32_t wi = cur.pos >> 3, off = cur.pos & 7u, p = wi << 3;
-    const uint32_t word = a.nib[(size_t)wi * a.nr + r];
+    const uint32_t off = cur.pos & 7u, p = wi << 3;
     bool run = true;
     int mode = 0;
 #pragma unroll
@@ -312,20 +320,21 @@ MSIM_HD int sp_word(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur
         const uint32_t pj = p + j;
         bool act = run & (j >= off) & (pj < cur.B);
         const uint32_t k = (word >> (4 * j)) & 15u;
-        const bool isc = act & (pj == cur.c0);
-        if (vote(isc)) {
-            if (isc) {
-                const bool ok = (mc.w == 0u) & ((cur.w0 >> 5) > (uint32_t)env.prop_tab(k < (uint32_t)M ? k : 0u));
-                if (ok) {
-                    sp_pop(a, r, cur);
-                } else {
-                    run = false;
-                    act = false;
-                    mode = 1;
-                    cur.pos = pj;
-                }
+        const bool cand = act & (((mA >> j) & 1u) != 0u);
+#if SP_DIAG_NOENG
+        const bool need = false;
+#else
+        const bool need = cand & (k < (uint32_t)M) & ((((mB >> j) & 1u) != 0u) | (mc.w != 0u));
+#endif
+        if (vote(need)) {
+            if (need) {
+                run = false;
+                act = false;
+                mode = 1;
+                cur.pos = pj;
             }
         }
+        cur.ci += (cand & act) ? 1u : 0u;  // a candidate the settled form takes
         if (act & (k >= (uint32_t)M)) {  // PickFinder fell through (simulation.h:220 asserts)
             cur.err |= SERR_PICK;
             run = false;
@@ -338,6 +347,27 @@ MSIM_HD int sp_word(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur
         cur.pos = p + 8 < cur.B ? p + 8 : cur.B;
         if (cur.pos == cur.B) mode = (int64_t)cur.TB >= D ? 6 : 4;
     }
+    return mode;
+}
+
+// One 32-block chunk of a lane in the nibble form (from pos to the chunk's end; the four words of cur.A in
+// order), then the next chunk moves up and the one after it is loaded. Returns the lane's mode (sp_word).
+template <int M, class Env, class Vote>
+MSIM_HD int sp_chunk(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur, SelMacro<M> &mc, uint32_t sid,
+                     int64_t D)
+{
+    if (cur.pos >= (cur.sg + 1) * a.seg) {  // segments start at chunk boundaries (seg is a multiple of GROUP)
+        cur.Tseg += a.segsum[(size_t)cur.sg * a.nr + r];
+        cur.sg++;
+        cur.ci = 0;
+    }
+    const uint32_t c = cur.pos >> 5;
+    int mode = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        if ((mode == 0) & ((cur.pos >> 3) == c * 4 + j))
+            mode = sp_word<M>(vote, cur, mc, sid, D, cur.A[j], (cur.mA.a >> (8 * j)) & 0xFFu,
+                              (cur.mA.b >> (8 * j)) & 0xFFu, c * 4 + j);
     if (vote(mc.F - mc.Ff >= 0xF000u)) {  // stp's 16-bit fields: flush well before they could overflow
         if (mc.F - mc.Ff >= 0xF000u) mc.flush_stale(env, sid);
     }
@@ -345,7 +375,12 @@ MSIM_HD int sp_word(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur
         cur.err |= SERR_SP;
         mode = 3;
     }
-    if (cur.err && mode != 3) mode = 3;
+    if (mode == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur.A[j] = cur.N[j];
+        cur.mA = cur.mN;
+        sp_chunk_at(a, r, c + 2, cur.N, cur.mN);
+    }
     return mode;
 }
 
@@ -353,16 +388,16 @@ MSIM_HD int sp_word(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur
 // RNG states, which tracks the block the engine has pending. Every block below B the engine consumes (the
 // pending block at each next(): the reference's loop draws the next find right after FoundBlock, main.cpp:
 // 153-157) was counted by K1, so its count is taken back here (msim_selpipe.h header).
-// Holds the FIFO by value and a copy of the counter access (device: SelDevEnv, a few pointers; host: a
-// forwarding reference type): a member reference would take the FIFO's address and keep it in scratch.
-template <class Fifo, class Env>
+// Holds the FIFO by value and the lane's found-counter access (Cnt: add(k, v) on C_F; device: one LDS pointer):
+// a member reference would take the FIFO's address and keep it in scratch.
+template <class Fifo, class Cnt>
 struct SpSrc {
     Fifo f;
-    Env env;
+    Cnt cnt;
     uint32_t pidx, pk, B;  // pending block and its finder (pidx = SP_NONE once the lane draws); the switch block
     MSIM_HD bool next(uint32_t &I, uint32_t &k)
     {
-        if (pidx < B) env.add(C_F, pk, 0xFFFFFFFFu);
+        if (pidx < B) cnt.add(pk, 0xFFFFFFFFu);
         f.next(I, k);
         if (pidx != SP_NONE) pidx += 1;
         pk = k;
@@ -372,32 +407,36 @@ struct SpSrc {
     MSIM_HD void settle() {}
 };
 
-// A lane leaves the nibble form for the engine: mode 1 (its candidate cur.c0 needs the engine: the FIFO is
-// seeded from the candidate's list entry) or mode 4 (it reached B with T_B < D: the FIFO is seeded by redrawing
-// B's group from its record). The settled state is handed to the engine (msim_selm.h to_exact). Returns the
-// new mode (2: engine, 3: error in cur.err). src: SpSrc (its FIFO, the pending block and finder).
+// A lane leaves the nibble form for the engine: mode 1 (its candidate at cur.pos needs the engine: the FIFO is
+// seeded from the candidate's list entry, found through the segment's slots) or mode 4 (it reached B with
+// T_B < D: the FIFO is seeded by redrawing B's super-group from its record). The settled state is handed to the
+// engine (msim_selm.h to_exact). Returns the new mode (2: engine, 3: error in cur.err). src: SpSrc.
 template <int M, class Src, class SelT, class Env>
 MSIM_HD int sp_enter(const SpArgs &a, uint32_t r, int mode, SpCur &cur, SelMacro<M> &mc, Src &src, SelT &s, Env &env,
                      uint32_t m, const uint32_t *sids)
 {
     auto &fifo = src.f;
     if (mode == 1) {
-        const EpEntry &e = a.list[cur.i0];
+        const uint32_t idx = a.slots[((size_t)cur.sg * a.cap + cur.ci) * a.nr + r];
+        if (idx >= a.lcap || a.list[idx].block != cur.pos) {
+            cur.err |= SERR_SP;  // the list overflowed (its entry was not stored)
+            return 3;
+        }
+        const EpEntry &e = a.list[idx];
         mc.T = (int64_t)(cur.Tseg + e.offset);
         mc.k = e.w0 & 31u;
         fifo.d.ri = e.ri;
         fifo.d.rp = e.rp;
         fifo.I0 = e.w1 >> 5;
         fifo.k0 = e.w1 & 31u;
-        src.pidx = cur.c0;
+        src.pidx = cur.pos;
     } else {
-        const uint32_t jb = cur.gE / a.gps, g = cur.gE % a.gps;
         const GroupRec gr = a.grec[(size_t)cur.gE * a.nr + r];
         fifo.d.ri = gr.ri;
         fifo.d.rp = gr.rp;
         uint32_t I = gr.w0 >> 5, k = gr.w0 & 31u;  // the group's first block
         uint32_t kB = k;
-        for (uint32_t b = (a.band_lo + jb) * a.seg + g * GROUP; b <= cur.B; ++b) {  // draws up to block B + 1
+        for (uint32_t b = sp_sg_block(a, cur.gE); b <= cur.B; ++b) {  // draws up to block B + 1
             kB = k;
             fifo.d.draw(I, k);
         }

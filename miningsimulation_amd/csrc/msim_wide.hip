@@ -9,6 +9,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "msim_jump.h"
 #include "msim_wide_launch.h"
 
@@ -566,7 +570,8 @@ static size_t w1_waves_per_cu(uint32_t m)
         return 0;
     return (size_t)blocks * R;
 }
-uint32_t wide_w1_runs(uint32_t m)
+// Depends only on (device, m): cached, since launch_wide asks on every launch (four occupancy queries).
+static uint32_t wide_w1_runs_uncached(uint32_t m)
 {
     const size_t w[4] = {w1_waves_per_cu<1>(m), w1_waves_per_cu<2>(m), w1_waves_per_cu<4>(m), w1_waves_per_cu<8>(m)};
     uint32_t best = 1;
@@ -581,6 +586,20 @@ uint32_t wide_w1_runs(uint32_t m)
         if ((r == 1 || r == 2 || r == 4 || r == 8) && wide_w1_lds(m, r) <= 150 * 1024) best = r;
     }
     return best;
+}
+uint32_t wide_w1_runs(uint32_t m)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, uint32_t>, uint32_t> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_pair(dev, m);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    const uint32_t r = wide_w1_runs_uncached(m);
+    cache[key] = r;
+    return r;
 }
 size_t wide_w3_lds(uint32_t m, uint32_t rcap, uint32_t nch)
 {

@@ -32,7 +32,7 @@ struct HostCtx {
     bool vote(bool s) const { return s; }
     void quad() {}
     void quad_done(uint32_t, uint32_t) {}
-    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
+    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp, uint32_t)
     {
         if (!s) return;
         const uint32_t idx = (uint32_t)list->size();
@@ -133,8 +133,9 @@ int run_pipeline(const SimParams &p, const uint64_t *perc, const int64_t *prop, 
     a.list_count = &count;
     a.recs = recs.data();
     for (uint32_t i = 0; i < count; ++i) {
-        if (L.k2_lean) episode_entry<M, true>(p, a, i);
-        else episode_entry<M, false>(p, a, i);
+        if (L.k2_kind == 0) episode_entry<M, 0>(p, a, i);
+        else if (L.k2_kind == 1) episode_entry<M, 1>(p, a, i);
+        else episode_entry<M, 2>(p, a, i);
     }
     for (uint32_t r = 0; r < n; ++r) {
         uint32_t F[M], S[M];

@@ -18,9 +18,10 @@ namespace {
 
 struct NibCtx {
     PipeLayout L;
-    uint32_t r, seg, jb, nsl = 0, nibw = 0;
+    uint32_t r, seg, jb, ps, nsl = 0, nibw = 0, ma = 0, mb = 0;
     uint32_t cnt[CNT_WORDS] = {0};
-    std::vector<uint32_t> *slots, *gsum, *gcum, *nib;
+    std::vector<uint32_t> *slots, *gcum, *nib;
+    std::vector<CMask> *cmask;
     std::vector<uint64_t> *gend;
     std::vector<GroupRec> *grec;
     std::vector<EpEntry> *list;
@@ -34,11 +35,18 @@ struct NibCtx {
     void quad() {}
     void quad_done(uint32_t g, uint32_t q4)
     {
-        if (q4 & 1u) (*nib)[((size_t)seg * (L.seg / 8) + g * (GROUP / 8) + (q4 >> 1)) * L.nr + r] = nibw;
+        if (q4 & 1u) (*nib)[sp_nib_index(L.nr, r, seg * (L.seg / 8) + g * (GROUP / 8) + (q4 >> 1))] = nibw;
+        if (q4 == GROUP / K1_QB - 1) {
+            (*cmask)[((size_t)seg * (L.seg / GROUP) + g) * L.nr + r] = CMask{ma, mb};
+            ma = mb = 0;
+        }
     }
-    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
+    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp,
+              uint32_t fthr)
     {
         if (!s) return;
+        ma |= 1u << (block & (GROUP - 1u));
+        if ((w1 >> 5) + ps < fthr) mb |= 1u << (block & (GROUP - 1u));
         const uint32_t idx = (uint32_t)list->size();
         if (idx < L.lcap) list->push_back(EpEntry{r, block, offset, w0, w1, {0, 0}, ri, rp});
         if (nsl < L.cap) (*slots)[((size_t)seg * L.cap + nsl) * L.nr + r] = idx;
@@ -46,12 +54,13 @@ struct NibCtx {
     }
     void group_start(uint32_t g, uint32_t w0, const Rng &ri, const Rng &rp)
     {
-        (*grec)[((size_t)jb * L.gps + g) * L.nr + r] = GroupRec{ri, rp, w0, 0};
-        for (uint32_t w = 0; w < CNT_WORDS; ++w) (*gcum)[(((size_t)jb * L.gps + g) * CNT_WORDS + w) * L.nr + r] = cnt[w];
+        if (g % SGROUP) return;  // records per super-group (as msim_drawgen.hip DevCtx<true>)
+        const size_t gi = (size_t)jb * L.nsg + g / SGROUP;
+        (*grec)[gi * L.nr + r] = GroupRec{ri, rp, w0, 0};
+        for (uint32_t w = 0; w < CNT_WORDS; ++w) (*gcum)[(gi * CNT_WORDS + w) * L.nr + r] = cnt[w];
     }
-    void group(uint32_t g, uint32_t sum, uint64_t end)
+    void group(uint32_t g, uint32_t, uint64_t end)
     {
-        (*gsum)[((size_t)jb * L.gps + g) * L.nr + r] = sum;
         if (g % SGROUP == SGROUP - 1 || g + 1 == L.gps) (*gend)[((size_t)jb * L.nsg + g / SGROUP) * L.nr + r] = end;
     }
 };
@@ -93,9 +102,9 @@ struct HostDraw {
     void fix(uint32_t &, uint32_t &) {}
 };
 using Fifo = SelFifo<HostDraw>;
-struct EnvRef {  // SpSrc's counter access on the host: the lane's one HostEnv
+struct EnvRef {  // SpSrc's found-counter access on the host: the lane's one HostEnv
     HostEnv *e;
-    void add(int a, uint32_t k, uint32_t v) { e->add(a, k, v); }
+    void add(uint32_t k, uint32_t v) { e->add(C_F, k, v); }
 };
 
 struct Stats {
@@ -120,10 +129,14 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
     build_pick_table_sp(perc, prop, self, M, &pick);
     build_log_table(&logt);
     build_jump_table(L.nseg, L.seg, jump.data());
-    std::vector<GroupRec> grec((size_t)L.nband * L.gps * n);
+    std::vector<GroupRec> grec((size_t)L.nband * L.nsg * n);
     std::vector<uint32_t> segcnt((size_t)L.nseg * CNT_WORDS * n), nslow((size_t)L.nseg * n),
-        slots((size_t)L.nseg * L.cap * n, 0xFFFFFFFFu), gsum((size_t)L.nband * L.gps * n),
-        gcum((size_t)L.nband * L.gps * CNT_WORDS * n), nib((size_t)L.nb / 8 * n);
+        slots((size_t)L.nseg * L.cap * n, 0xFFFFFFFFu),
+        gcum((size_t)L.nband * L.nsg * CNT_WORDS * n), nib((size_t)L.nb / 8 * n);
+    std::vector<CMask> cmask((size_t)L.nb / 32 * n);
+    uint32_t ps = 0;
+    for (int k = 0; k < M; ++k)
+        if (self[k]) ps = (uint32_t)prop[k];
     std::vector<uint64_t> segsum((size_t)L.nseg * n), gend((size_t)L.nband * L.nsg * n);
     std::vector<EpEntry> list;
     for (uint32_t r = 0; r < n; ++r) {
@@ -146,11 +159,12 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
             cx.jb = j - L.band_lo;
             cx.grec = &grec;
             cx.slots = &slots;
-            cx.gsum = &gsum;
             cx.gend = &gend;
             cx.gcum = &gcum;
             cx.list = &list;
             cx.nib = &nib;
+            cx.cmask = &cmask;
+            cx.ps = ps;
             segsum[(size_t)j * n + r] = draw_segment<NibCtx, true>(cx, ri, rp, &logt, &pick, j * L.seg, L.seg, j >= L.band_lo);
             for (uint32_t w = 0; w < CNT_WORDS; ++w) segcnt[((size_t)j * CNT_WORDS + w) * n + r] = cx.cnt[w];
             nslow[(size_t)j * n + r] = cx.nsl;
@@ -159,7 +173,6 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
     SpArgs a;
     a.nr = n;
     a.seg = L.seg;
-    a.gps = L.gps;
     a.nsg = L.nsg;
     a.nseg = L.nseg;
     a.nb = L.nb;
@@ -170,12 +183,12 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
     a.segcnt = segcnt.data();
     a.nslow = nslow.data();
     a.slots = slots.data();
-    a.gsum = gsum.data();
     a.gend = gend.data();
     a.gcum = gcum.data();
     a.grec = grec.data();
     a.list = list.data();
     a.nib = nib.data();
+    a.cmask = cmask.data();
     uint64_t cum[MAXM];
     uint64_t c = 0;
     uint32_t sids[SEL_MAXS] = {SEL_NONE, SEL_NONE, SEL_NONE, SEL_NONE};
@@ -205,7 +218,7 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
         src.f.d.cum = cum;
         src.f.d.m = M;
         src.f.n = 0;
-        src.env = EnvRef{&env};
+        src.cnt = EnvRef{&env};
         src.pidx = SP_NONE;
         src.pk = 0;
         src.B = cur.B;
@@ -215,7 +228,7 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
         while (mode != 3) {
             if (mode == 0) {
                 ++g_st.words;
-                mode = sp_word<M>(a, r, env, [](bool b) { return b; }, cur, mc, sid, D);
+                mode = sp_chunk<M>(a, r, env, [](bool b) { return b; }, cur, mc, sid, D);
             } else if (mode == 6) {
                 mc.finish(env, sid, out);
                 mode = 3;

@@ -46,7 +46,8 @@ def test_config_validation_without_gpu(msim_lib_path):
         ([Miner(0, 60, 1000), Miner(1, 30, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 90
         ([Miner(0, 60, 1000), Miner(1, 50, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 110
         # one run's explicit chains above 8 GiB on the general engine (20 000 miners x ~55 k blocks)
-        ([Miner(k, 1 if k < 100 else 0, 1000) for k in range(20000)], _lib.MSIM_E_MINERS),
+        # a selfish network whose one G lane (every block of every miner's chain) exceeds 96 GiB
+        ([Miner(k, 1 if k < 100 else 0, 1000, k == 0) for k in range(160000)], _lib.MSIM_E_MINERS),
         ([Miner(0, 50, -1), Miner(1, 50, 1000)], _lib.MSIM_E_INVALID),
     ]
     for miners, code in bad:
@@ -83,20 +84,26 @@ def test_config_validation_without_gpu(msim_lib_path):
     assert big.workspace_bytes(65536) < 3 * 2**30, big.workspace_bytes(65536)
     # configs[2] at its per-GPU size: the selfish pipeline (msim_selpipe.h) keeps K1's per-block finder nibbles,
     # candidate list and band records (~34 KB per run-year, ~4.5 GB of the 288 GB); E1 alone stays under 1 GiB
-    c3 = Simulation(setup_miners(1000, selfish_perc=40))
-    assert c3.pipeline_info(131072)["uses_pipeline"] == 5
-    assert c3.workspace_bytes(131072) < 6 * 2**30, c3.workspace_bytes(131072)
+    # (opt-in: MSIM_SELPIPE=1; E1 serves configs[2] by default)
     import os
-    os.environ["MSIM_NO_SELPIPE"] = "1"
+    e1 = Simulation(setup_miners(1000, selfish_perc=40))
+    assert e1.pipeline_info(131072)["uses_pipeline"] == 3
+    assert e1.workspace_bytes(131072) < 2**30
+    os.environ["MSIM_SELPIPE"] = "1"
     try:
-        e1 = Simulation(setup_miners(1000, selfish_perc=40))
-        assert e1.pipeline_info(131072)["uses_pipeline"] == 3
-        assert e1.workspace_bytes(131072) < 2**30
+        c3 = Simulation(setup_miners(1000, selfish_perc=40))
+        assert c3.pipeline_info(131072)["uses_pipeline"] == 5
+        assert c3.workspace_bytes(131072) < 8 * 2**30, c3.workspace_bytes(131072)
     finally:
-        del os.environ["MSIM_NO_SELPIPE"]
+        del os.environ["MSIM_SELPIPE"]
     # the large-network path (msim_wide.h): more than 15 honest miners, or integer weights
     assert Simulation([Miner(k, 7 if k < 10 else 5, 1000) for k in range(16)]).wide
     assert not Simulation(setup_miners()).wide
+    # an honest network on G sizes its windows to 4 096 blocks (honest forks fold far inside it):
+    # 20 000 miners fit, and the workspace stays at the 2 GiB window budget
+    huge = Simulation([Miner(k, 1 if k < 100 else 0, 1000) for k in range(20000)])
+    assert huge.pipeline_info(1024)["uses_pipeline"] == 4
+    assert huge.workspace_bytes(65536) < 3 * 2**30, huge.workspace_bytes(65536)
     c5 = [Miner(k, w, 1000) for k, w in enumerate([30720, 29696] + [41] * 1024)]
     assert Simulation(c5, total_weight=102400).wide
     for miners, W, code in (

@@ -15,6 +15,12 @@ DAY = 86_400_000
 C3 = ([40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [1] + [0] * 8)
 
 
+@pytest.fixture(autouse=True)
+def _selpipe_on(monkeypatch):
+    """The selfish pipeline is opt-in (msim_api.hip: E1 serves configs[2] by default)."""
+    monkeypatch.setenv("MSIM_SELPIPE", "1")
+
+
 @pytest.fixture(scope="module")
 def msim(msim_lib_path):
     import torch
