@@ -35,7 +35,7 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 
 
 # PMC constants of the dominant kernel per launch at the default run counts, from rocprofv3 --pmc passes of
-# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc.sh: FETCH_SIZE, WRITE_SIZE and the SQ
+# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc_r05.sh: FETCH_SIZE, WRITE_SIZE and the SQ
 # set in separate passes; the files hold values summed over the 2 launches, KB). PMC counters cannot be collected
 # inside the timed process: these are the recorded values of the same kernel, and every field computed from them
 # names its file.

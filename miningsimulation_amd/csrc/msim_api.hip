@@ -527,6 +527,11 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
         sa.list = da.list;
         sa.nib = da.nib;
         sa.cmask = da.cmask;
+        sa.stale = (uint32_t *)(pw + sp->SL.stale_off);
+        // engine phases start when 48 of a wave's 64 lanes wait (measured on configs[2]: 16 -> 88.9 ms,
+        // 32 -> 77.8, 48 -> 77.1 per 131 072-run step, profiles/r05/sp); MSIM_SP_XTH overrides (A/B)
+        sa.xth = 48;
+        if (const char *e = getenv("MSIM_SP_XTH")) sa.xth = (uint32_t)atoi(e);
         a.plist = groups[0].plist;
         a.nlist = 1;
         a.uni = groups[0].uni;
@@ -536,7 +541,9 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
             a.sn = sn;
             da.run_begin = run_begin + s0;
             da.n = sn;
-            if (hipMemsetAsync(da.list_count, 0, sizeof(uint32_t), s) != hipSuccess) return MSIM_E_HIP;
+            if (hipMemsetAsync(da.list_count, 0, sizeof(uint32_t), s) != hipSuccess ||
+                hipMemsetAsync(sa.stale, 0, (size_t)L.nb / 32 * L.nr * 4, s) != hipSuccess)
+                return MSIM_E_HIP;
             event(k1_events);
             if (launch_draws(da, s) != hipSuccess) return MSIM_E_HIP;
             event(k1_events);

@@ -49,6 +49,7 @@ constexpr uint32_t SP_NONE = 0xFFFFFFFFu;
 constexpr double SP_MAX_RHO = 0.02;  // candidate rate above which E1 (in-lane draws) serves the network
 enum : uint32_t { SERR_SP = 128u };  // the pipeline's capacities (slots, list, band): recomputed by E2
 
+
 // P(block is a candidate) = sum over honest k of share_k * P(I_next <= prop_k + prop_s).
 inline double sp_rho(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int m)
 {
@@ -65,19 +66,20 @@ inline double sp_rho(const uint64_t *perc, const int64_t *prop, const uint8_t *s
 // The honest pipeline's layout (msim_pipeline.h) sized for the candidate rate, plus the nibbles.
 struct SpLayout {
     PipeLayout L;
-    size_t nib_off, cmask_off, total;
+    size_t nib_off, cmask_off, stale_off, total;
 };
 inline SpLayout sp_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget,
                               uint32_t slots)
 {
     SpLayout s;
     const double mu = (double)duration_ms / 599999.5;
-    // >= nb / 2 bytes of nibbles and nb / 4 bytes of candidate masks per run
-    const double nib = (mu + 8.0 * sqrt(mu > 1.0 ? mu : 1.0) + 64.0 + GROUP * 256.0) * 0.75;
+    // >= nb / 2 bytes of nibbles, nb / 4 of candidate masks and nb / 8 of stale masks per run
+    const double nib = (mu + 8.0 * sqrt(mu > 1.0 ? mu : 1.0) + 64.0 + GROUP * 256.0) * 0.875;
     s.L = pipe_layout_for(rho, m, duration_ms, n_runs, budget, slots, false, nib);
     s.nib_off = (s.L.total + 255) / 256 * 256;
     s.cmask_off = s.nib_off + ((size_t)s.L.nb / 8 * s.L.nr * 4 + 255) / 256 * 256;
-    s.total = s.cmask_off + ((size_t)s.L.nb / 32 * s.L.nr * 8 + 255) / 256 * 256;
+    s.stale_off = s.cmask_off + ((size_t)s.L.nb / 32 * s.L.nr * 8 + 255) / 256 * 256;
+    s.total = s.stale_off + ((size_t)s.L.nb / 32 * s.L.nr * 4 + 255) / 256 * 256;
     return s;
 }
 
@@ -121,10 +123,24 @@ struct SpArgs {
     const EpEntry *list;
     const uint32_t *nib;     // [nb/32][nr][4]: word w (blocks 8w .. 8w+7) of run r at ((w >> 2) * nr + r) * 4 + (w & 3)
     const CMask *cmask;      // [nb/32][nr]: per chunk (A: listed candidates, B: candidates with I_next <= prop_k)
+    uint32_t *stale;         // [nb/32][nr]: S2's stale honest blocks per chunk (zeroed before S2; SpSt)
+    uint32_t xth;            // waiting lanes that start an engine phase (msim_sel_kernels.hip msim_selpipe_kernel)
 };
+
 
 // The u32 index of nibble word w of run r (the 16-byte chunk layout above; K1 writes it, S2 reads it).
 MSIM_HD size_t sp_nib_index(uint32_t nr, uint32_t r, uint32_t w) { return ((size_t)(w >> 2) * nr + r) * 4 + (w & 3u); }
+
+// Chunks the nibble form keeps loaded: a ring of SP_PF, the chunk at ring slot S being the one the lane's S-th
+// table step (mod SP_PF) since the last refill reads. All lanes of a nibble phase step together and every phase
+// starts from a refill, so the slot is wave-uniform and each step names its registers at compile time: a ring
+// shifted by register moves made the compiler wait for the load just issued (a move of a pending load's
+// destination), which left every chunk waiting on memory (measured: ~18k cycles per chunk).
+#ifndef MSIM_SP_PF
+#define MSIM_SP_PF 4
+#endif
+constexpr int SP_PF = MSIM_SP_PF;
+static_assert(SP_PF == 1 || SP_PF == 2 || SP_PF == 4, "the kernel steps four ring slots per pass");
 
 // The nibble-form cursor of one run (saved to LDS around engine phases on the device).
 struct SpCur {
@@ -136,8 +152,8 @@ struct SpCur {
     uint64_t TB;           // T_B
     uint32_t gE;           // band position of B's super-group: jb * nsg + q
     uint32_t err;
-    uint32_t A[4], N[4];   // the nibble chunk of pos (blocks 32c .. 32c + 31) and the next one, loaded ahead
-    CMask mA, mN;          // their candidate masks (not saved with the cursor: reloaded, sp_refill)
+    uint32_t A[SP_PF][4];  // the nibble chunk of pos (blocks 32c .. 32c + 31) and the next ones, loaded ahead
+    CMask mA[SP_PF];       // their candidate masks (not saved with the cursor: reloaded, sp_refill)
     static constexpr int NW = 10;
     MSIM_HD void save(uint32_t *p, int st) const
     {
@@ -158,6 +174,52 @@ struct SpCur {
         err = p[9 * st];
     }
 };
+
+// The settled state of a run in the nibble form: msim_selm.h's (F, h, w) and unflushed selfish stale blocks,
+// with the honest branch kept as a block RANGE instead of per-miner counts. Every honest block the nibble form
+// applies after the last resolution is in the honest branch, so the branch is the honest blocks of
+// [prs, pos) (plus, after an engine hand-back, the blocks the engine handed over: their per-miner counts wait
+// in the lane's C_A counters, pxf). When the selfish branch wins (an honest find at w == 2) those blocks are
+// stale: they are marked in a per-chunk bit mask (smask for the current chunk, SpArgs::stale for the chunks
+// behind it) and counted per miner once, at the end of the run (sp_stale_counts). No per-miner state is
+// touched per block, which is what lets four blocks at a time go through one table entry (sp_lut_entry).
+struct SpSt {
+    uint32_t F, h, w, sst;
+    uint32_t prs;     // first block of the honest branch's range
+    uint32_t pxf;     // the branch also holds engine-handed blocks (C_A)
+    uint32_t smask;   // stale honest blocks of chunk schunk marked so far (bit i: block 32 schunk + i)
+    uint32_t schunk;
+    uint32_t hbits;   // honest blocks of chunk schunk the form has applied
+    static constexpr int NW = 9;
+    MSIM_HD void save(uint32_t *p, int st) const
+    {
+        const uint32_t v[NW] = {F, h, w, sst, prs, pxf, smask, schunk, hbits};
+#pragma unroll
+        for (int i = 0; i < NW; ++i) p[i * st] = v[i];
+    }
+    MSIM_HD void load(const uint32_t *p, int st)
+    {
+        F = p[0];
+        h = p[st];
+        w = p[2 * st];
+        sst = p[3 * st];
+        prs = p[4 * st];
+        pxf = p[5 * st];
+        smask = p[6 * st];
+        schunk = p[7 * st];
+        hbits = p[8 * st];
+    }
+};
+
+// Nibble-lsb bits (bit 4i) of the nibbles of `word` equal to k.
+MSIM_HD uint32_t sp_nibeq(uint32_t word, uint32_t k)
+{
+    const uint32_t x = word ^ (k * 0x11111111u);
+    return ~(x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u;
+}
+// Nibble-lsb bits of one half word (bits 0, 4, 8, 12) packed to bits 0..3: the four partial products of
+// z * 0x1248 land on distinct bit positions (no carries), bits 12..15 holding the packed value.
+MSIM_HD uint32_t sp_pack4(uint32_t z) { return (((z & 0x1111u) * 0x1248u) >> 12) & 15u; }
 
 // Nibble chunk c (blocks 32c .. 32c + 31) of run r and its candidate masks (one 16-byte and one 8-byte load);
 // beyond the pre-generated blocks, the last chunk.
@@ -184,12 +246,19 @@ MSIM_HD uint32_t sp_nib(const SpArgs &a, uint32_t r, uint32_t b)
     return (a.nib[sp_nib_index(a.nr, r, b >> 3)] >> (4 * (b & 7u))) & 15u;
 }
 
-// Load the chunk of pos and the next one (the nibble form reads a chunk per 32 blocks with the next one in
-// flight, so its latency is hidden).
+// Load the chunk of pos and the SP_PF - 1 after it (the nibble form reads a chunk per 32 blocks with the next
+// ones in flight, so their latency is hidden).
 MSIM_HD void sp_refill(const SpArgs &a, uint32_t r, SpCur &c)
 {
-    sp_chunk_at(a, r, c.pos >> 5, c.A, c.mA);
-    sp_chunk_at(a, r, (c.pos >> 5) + 1, c.N, c.mN);
+#pragma unroll
+    for (int i = 0; i < SP_PF; ++i) sp_chunk_at(a, r, (c.pos >> 5) + (uint32_t)i, c.A[i], c.mA[i]);
+}
+
+// Bits [lo, hi) of a chunk word (lo <= hi <= 32).
+MSIM_HD uint32_t sp_bits(uint32_t lo, uint32_t hi)
+{
+    const uint32_t up = hi >= 32u ? 0xFFFFFFFFu : ((1u << hi) - 1u);
+    return lo >= 32u ? 0u : up & ~((1u << lo) - 1u);
 }
 
 // Candidates of run r among blocks [b0, b1) (their A mask bits; the chunks loaded here: rare paths only).
@@ -197,10 +266,8 @@ MSIM_HD uint32_t sp_count_cands(const SpArgs &a, uint32_t r, uint32_t b0, uint32
 {
     uint32_t n = 0;
     for (uint32_t c = b0 >> 5; c * 32 < b1; ++c) {
-        uint32_t m = a.cmask[(size_t)c * a.nr + r].a;
         const uint32_t lo = b0 > c * 32 ? b0 - c * 32 : 0u, hi = b1 < c * 32 + 32 ? b1 - c * 32 : 32u;
-        m &= (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-        n += (uint32_t)__builtin_popcount(m);
+        n += (uint32_t)__builtin_popcount(a.cmask[(size_t)c * a.nr + r].a & sp_bits(lo, hi));
     }
     return n;
 }
@@ -218,7 +285,6 @@ MSIM_HD void sp_seek(const SpArgs &a, uint32_t r, SpCur &c, uint32_t pos)
     }
     c.ci += sp_count_cands(a, r, from, pos);
     c.pos = pos;
-    sp_refill(a, r, c);
 }
 
 // First block of band super-group gE.
@@ -293,68 +359,225 @@ MSIM_HD void sp_counts(const SpArgs &a, uint32_t r, const SpCur &c, uint32_t (&F
     const uint32_t jb = c.gE / a.nsg;
     for (uint32_t s = 0; s < a.band_lo + jb; ++s) add_packed<M>(F, a.segcnt + (size_t)s * CNT_WORDS * a.nr + r, a.nr);
     add_packed<M>(F, a.gcum + (size_t)c.gE * CNT_WORDS * a.nr + r, a.nr);
-    for (uint32_t b = sp_sg_block(a, c.gE); b < c.B; ++b) {
-        const uint32_t k = sp_nib(a, r, b);
+    // the super-group's blocks before B, a word at a time (eight loads in flight per batch)
+    const uint32_t b0 = sp_sg_block(a, c.gE);
+    for (uint32_t w0 = b0 >> 3; w0 * 8 < c.B; w0 += 8) {
+        uint32_t wd[8];
 #pragma unroll
-        for (int kk = 0; kk < M; ++kk) F[kk] += (uint32_t)kk == k ? 1u : 0u;
-    }
-}
-
-// One nibble word (blocks 8 wi .. 8 wi + 7) of a lane in the nibble form: the settled-state transition of every
-// block from max(pos, 8 wi) up to the word's end or B, from the block's finder and candidate bits alone
-// (mA, mB: the word's bits of the chunk masks; a block whose finder fell through PickFinder is left to the
-// error check). A candidate settles (msim_selm.h step: an honest find settles
-// iff I_next > prop_k + (w ? prop_s : 0); a candidate has I_next <= prop_k + prop_s) iff its B bit is clear
-// and w == 0. Returns the lane's mode: 0 (continue), 1 (cur.pos is a candidate that needs the engine), 4
-// (cur.pos == B: to the engine, T_B < D), 6 (the run ends after block B - 1: T_B >= D, finish the settled
-// form), 3 (error in cur.err). vote(b): nonzero when b holds for some lane of the wave (host: b).
-template <int M, class Vote>
-MSIM_HD int sp_word(Vote vote, SpCur &cur, SelMacro<M> &mc, uint32_t sid, int64_t D, uint32_t word,
-                    uint32_t mA, uint32_t mB, uint32_t wi)
-{
-    const uint32_t off = cur.pos & 7u, p = wi << 3;
-    bool run = true;
-    int mode = 0;
+        for (uint32_t q = 0; q < 8; ++q) wd[q] = (w0 + q) * 8 < c.B ? a.nib[sp_nib_index(a.nr, r, w0 + q)] : 0u;
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        const uint32_t pj = p + j;
-        bool act = run & (j >= off) & (pj < cur.B);
-        const uint32_t k = (word >> (4 * j)) & 15u;
-        const bool cand = act & (((mA >> j) & 1u) != 0u);
-#if SP_DIAG_NOENG
-        const bool need = false;
-#else
-        const bool need = cand & (k < (uint32_t)M) & ((((mB >> j) & 1u) != 0u) | (mc.w != 0u));
-#endif
-        if (vote(need)) {
-            if (need) {
-                run = false;
-                act = false;
-                mode = 1;
-                cur.pos = pj;
+        for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t p = (w0 + q) * 8;
+            const uint32_t in = p < c.B ? sp_bits(0u, c.B - p < 8u ? c.B - p : 8u) : 0u;  // b0 is word-aligned
+#pragma unroll
+            for (int kk = 0; kk < M; ++kk) {
+                const uint32_t z = sp_nibeq(wd[q], (uint32_t)kk);
+                F[kk] += (uint32_t)__builtin_popcount((sp_pack4(z) | (sp_pack4(z >> 16) << 4)) & in);
             }
         }
-        cur.ci += (cand & act) ? 1u : 0u;  // a candidate the settled form takes
-        if (act & (k >= (uint32_t)M)) {  // PickFinder fell through (simulation.h:220 asserts)
-            cur.err |= SERR_PICK;
-            run = false;
-            act = false;
-            mode = 3;
-        }
-        mc.transition(k, k == sid, act, sid);
     }
-    if (run) {
-        cur.pos = p + 8 < cur.B ? p + 8 : cur.B;
-        if (cur.pos == cur.B) mode = (int64_t)cur.TB >= D ? 6 : 4;
-    }
-    return mode;
 }
 
-// One 32-block chunk of a lane in the nibble form (from pos to the chunk's end; the four words of cur.A in
-// order), then the next chunk moves up and the one after it is loaded. Returns the lane's mode (sp_word).
+
+// ---------------------------------------------------------------- the settled form over nibbles
+// The settled-form transitions (msim_selm.h SelMacro::transition) of four blocks with selfish pattern s4 (bit i:
+// block i is the selfish miner's; the others honest) from lead class cls (w = cls; cls 6 stands for any
+// w >= 6, from which no resolution can happen within four blocks), as one 27-bit table entry:
+//   bits 0-3   w after the four blocks (cls 6: the change + 4)
+//   bit 4      some resolution (honest find at w == 0: the honest branch wins; at w == 2: the selfish one)
+//   bit 5      the first resolution is a selfish win (the honest branch open before the half is stale)
+//   bits 6-8   ties since the last resolution (none: since the half's start)
+//   bits 9-12  F's increase beyond the entering h (which the first resolution adds)
+//   bits 13-15 selfish stale blocks beyond the entering h (which a first resolution by an honest win adds)
+//   bits 16-19 honest blocks of the half made stale by selfish wins
+//   bits 20-23 w != 0 before block i (a candidate there needs the engine)
+//   bits 24-26 one past the last resolution's block (0: none)
+MSIM_HD uint32_t sp_lut_entry(uint32_t cls, uint32_t s4)
+{
+    uint32_t w = cls, hrel = 0, rs = 0, fsw = 0, dF = 0, dsst = 0, st = 0, wnz = 0, lrs = 0, rstart = 0;
+    for (uint32_t i = 0; i < 4; ++i) {
+        if (w != 0) wnz |= 1u << i;
+        if ((s4 >> i) & 1u) {
+            w += 1;
+            continue;
+        }
+        if (w == 0 || w == 2) {
+            const bool res = w == 0;
+            dF += hrel + (res ? 1u : 2u);
+            if (res) dsst += hrel;
+            else
+                for (uint32_t j = rstart; j <= i; ++j)
+                    if (!((s4 >> j) & 1u)) st |= 1u << j;
+            if (!rs) fsw = res ? 0u : 1u;
+            rs = 1;
+            hrel = 0;
+            w = 0;
+            rstart = i + 1;
+            lrs = i + 1;
+        } else {
+            hrel += 1;
+            w -= 1;
+        }
+    }
+    const uint32_t wf = cls < 6 ? w : w + 4u - 6u;
+    return wf | (rs << 4) | (fsw << 5) | (hrel << 6) | (dF << 9) | (dsst << 13) | (st << 16) | (wnz << 20) | (lrs << 24);
+}
+constexpr int SP_LUT = 7 * 16;
+
+// The form moves to chunk c: the stale mask of the chunk it leaves is stored (SpArgs::stale starts zeroed, so
+// chunks with no stale block, and chunks the engine consumed, are never written).
+MSIM_HD void sp_to_chunk(const SpArgs &a, uint32_t r, SpSt &st, uint32_t c)
+{
+    if (st.schunk == c) return;
+    if (st.smask) a.stale[(size_t)st.schunk * a.nr + r] = st.smask;
+    st.schunk = c;
+    st.smask = 0;
+    st.hbits = 0;
+}
+
+// Honest blocks of [lo, 32 schunk) are stale (a selfish win whose honest branch began in an earlier chunk; rare):
+// their chunks' masks, already stored, get the bits.
+MSIM_HD void sp_mark_prev(const SpArgs &a, uint32_t r, const SpSt &st, uint32_t lo, uint32_t sid)
+{
+    for (uint32_t c = lo >> 5; c < st.schunk; ++c) {
+        uint32_t w[4];
+        CMask m;
+        sp_chunk_at(a, r, c, w, m);
+        uint32_t hb = 0;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t z = sp_nibeq(w[j], sid);
+            hb |= ((~(sp_pack4(z) | (sp_pack4(z >> 16) << 4))) & 0xFFu) << (8 * j);
+        }
+        hb &= sp_bits(lo > c * 32 ? lo - c * 32 : 0u, 32u);
+        if (hb) a.stale[(size_t)c * a.nr + r] |= hb;
+    }
+}
+
+// The honest branch's engine-handed blocks (C_A) at the first resolution after the hand-back: stale when the
+// selfish branch wins (moved to C_S, out of C_F), in the best chain otherwise.
+template <int M, class Env>
+MSIM_HD void sp_pend_resolve(Env &env, bool swin, SpSt &st)
+{
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t v = env.get(C_A, (uint32_t)j);
+        if (v) {
+            if (swin) {
+                env.add(C_S, (uint32_t)j, v);
+                env.add(C_F, (uint32_t)j, 0u - v);
+            }
+            env.set(C_A, (uint32_t)j, 0u);
+        }
+    }
+    st.pxf = 0;
+}
+
+// One block in the settled form, block by block (the paths around engine entries, hand-backs and B): a find
+// by k at block `pos` of chunk st.schunk (msim_selm.h SelMacro::transition, with the branch as a range).
+template <int M, class Env>
+MSIM_HD void sp_blk(const SpArgs &a, uint32_t r, Env &env, SpSt &st, uint32_t pos, uint32_t k, uint32_t sid)
+{
+    if (k == sid) {
+        st.w += 1;
+        return;
+    }
+    st.hbits |= 1u << (pos & 31u);
+    if ((st.w == 0u) | (st.w == 2u)) {
+        const bool sw = st.w == 2u;
+        if (sw) {  // the honest branch [prs, pos] is stale
+            const uint32_t c0 = st.schunk * 32;
+            if (st.prs < c0) sp_mark_prev(a, r, st, st.prs, sid);
+            st.smask |= st.hbits & sp_bits(st.prs > c0 ? st.prs - c0 : 0u, (pos & 31u) + 1u);
+        }
+        if (st.pxf) sp_pend_resolve<M>(env, sw, st);
+        st.F += st.h + (sw ? 2u : 1u);
+        st.sst += sw ? 0u : st.h;
+        st.h = 0;
+        st.w = 0;
+        st.prs = pos + 1;
+    } else {
+        st.h += 1;
+        st.w -= 1;
+    }
+}
+
+// The nibble form block by block from cur.pos to the end of its word: the word that the table path left
+// (a candidate that needs the engine, B, a finder that fell through PickFinder) or the rest of a word the
+// engine handed back in. Returns the lane's mode: 0 (word done: cur.pos at the next word), 1 (cur.pos is a
+// candidate that needs the engine: an honest find settles iff I_next > prop_k + (w ? prop_s : 0), a candidate
+// has I_next <= prop_k + prop_s, and its B bit says I_next <= prop_k), 4 (cur.pos == B, T_B < D: to the
+// engine), 6 (cur.pos == B, T_B >= D: the run ends after block B - 1), 3 (error in cur.err).
+template <int M, class Env>
+MSIM_HD int sp_slow_word(const SpArgs &a, uint32_t r, Env &env, SpCur &cur, SpSt &st, uint32_t sid, int64_t D)
+{
+    while (cur.pos >= (cur.sg + 1) * a.seg) {  // segments start at chunk boundaries
+        cur.Tseg += a.segsum[(size_t)cur.sg * a.nr + r];
+        cur.sg++;
+        cur.ci = 0;
+    }
+    sp_to_chunk(a, r, st, cur.pos >> 5);
+    const uint32_t wi = cur.pos >> 3, p = wi << 3;
+    const uint32_t word = a.nib[sp_nib_index(a.nr, r, wi)];
+    const CMask m = a.cmask[(size_t)(wi >> 2) * a.nr + r];
+    const uint32_t sh = 8u * (wi & 3u), mA = (m.a >> sh) & 0xFFu, mB = (m.b >> sh) & 0xFFu;
+    for (uint32_t j = cur.pos & 7u; j < 8; ++j) {
+        const uint32_t pj = p + j;
+        if (pj >= cur.B) {
+            cur.pos = cur.B;
+            return (int64_t)cur.TB >= D ? 6 : 4;
+        }
+        const uint32_t k = (word >> (4 * j)) & 15u;
+        if (k >= (uint32_t)M) {  // PickFinder fell through (simulation.h:220 asserts)
+            cur.pos = pj;
+            cur.err |= SERR_PICK;
+            return 3;
+        }
+        const bool cand = ((mA >> j) & 1u) != 0u;
+        if (cand & ((((mB >> j) & 1u) != 0u) | (st.w != 0u))) {
+            cur.pos = pj;
+            return 1;
+        }
+        cur.ci += cand ? 1u : 0u;  // a candidate that settles
+        sp_blk<M>(a, r, env, st, pj, k, sid);
+    }
+    cur.pos = p + 8;
+    return 0;
+}
+
+// Applies table entry e of a half word (lead class cls, selfish pattern s4) at chunk bit hoff / block hs. The
+// rare parts (a selfish win whose branch began in an earlier chunk, engine-handed blocks) go through vote(b)
+// (nonzero when b holds for some lane; host: b).
 template <int M, class Env, class Vote>
-MSIM_HD int sp_chunk(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cur, SelMacro<M> &mc, uint32_t sid,
-                     int64_t D)
+MSIM_HD void sp_apply(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpSt &st, uint32_t e, uint32_t cls, uint32_t s4,
+                      uint32_t hoff, uint32_t hs, uint32_t sid)
+{
+    const uint32_t rs = (e >> 4) & 1u, fsw = (e >> 5) & 1u, hl = (e >> 6) & 7u;
+    st.w = cls == 6u ? st.w + (e & 15u) - 4u : (e & 15u);
+    st.F += (rs ? st.h : 0u) + ((e >> 9) & 15u);
+    st.sst += ((rs & (fsw ^ 1u)) ? st.h : 0u) + ((e >> 13) & 7u);
+    st.h = rs ? hl : st.h + hl;
+    const uint32_t c0 = st.schunk * 32;
+    // a selfish win first: the honest branch open before the half, [prs, hs), is stale too
+    st.smask |= fsw ? st.hbits & sp_bits(st.prs > c0 ? st.prs - c0 : 0u, hoff) : 0u;
+    if (vote((fsw != 0u) & (st.prs < c0))) {
+        if (fsw && st.prs < c0) sp_mark_prev(a, r, st, st.prs, sid);
+    }
+    if (vote((rs != 0u) & (st.pxf != 0u))) {
+        if (rs && st.pxf) sp_pend_resolve<M>(env, fsw != 0u, st);
+    }
+    st.smask |= ((e >> 16) & 15u) << hoff;
+    st.hbits |= (~s4 & 15u) << hoff;
+    st.prs = rs ? hs + ((e >> 24) & 7u) : st.prs;
+}
+
+// The nibble form over the rest of cur's chunk (ring slot S), a whole word at a time: the word's selfish pattern, two table
+// entries (lut: SP_LUT entries, LDS on the device), and the word is applied when none of its candidates needs
+// the engine, it ends before B and no finder fell through; otherwise the lane stops at the word (mode 9: the
+// block-by-block path, sp_slow_word, runs it among the engine phase's lanes). At the chunk's end the next chunk
+// moves up and the one after it is loaded. Returns the lane's mode (0: continue, 9: a word for the slow path).
+template <int M, int S, class Env, class Vote>
+MSIM_HD int sp_chunk(const SpArgs &a, uint32_t r, Env &env, Vote vote, const uint32_t *lut, SpCur &cur, SpSt &st,
+                     uint32_t sid)
 {
     if (cur.pos >= (cur.sg + 1) * a.seg) {  // segments start at chunk boundaries (seg is a multiple of GROUP)
         cur.Tseg += a.segsum[(size_t)cur.sg * a.nr + r];
@@ -362,25 +585,37 @@ MSIM_HD int sp_chunk(const SpArgs &a, uint32_t r, Env &env, Vote vote, SpCur &cu
         cur.ci = 0;
     }
     const uint32_t c = cur.pos >> 5;
+    sp_to_chunk(a, r, st, c);
     int mode = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-        if ((mode == 0) & ((cur.pos >> 3) == c * 4 + j))
-            mode = sp_word<M>(vote, cur, mc, sid, D, cur.A[j], (cur.mA.a >> (8 * j)) & 0xFFu,
-                              (cur.mA.b >> (8 * j)) & 0xFFu, c * 4 + j);
-    if (vote(mc.F - mc.Ff >= 0xF000u)) {  // stp's 16-bit fields: flush well before they could overflow
-        if (mc.F - mc.Ff >= 0xF000u) mc.flush_stale(env, sid);
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t p = (c * 4 + j) * 8;
+        if ((mode == 0) & (cur.pos == p)) {
+            const uint32_t word = cur.A[S][j];
+            const uint32_t z = sp_nibeq(word, sid), s8 = sp_pack4(z) | (sp_pack4(z >> 16) << 4);
+            const uint32_t c0 = st.w < 6u ? st.w : 6u;
+            const uint32_t e0 = lut[c0 * 16 + (s8 & 15u)];
+            const uint32_t w1 = c0 == 6u ? st.w + (e0 & 15u) - 4u : (e0 & 15u);
+            const uint32_t c1 = w1 < 6u ? w1 : 6u;
+            const uint32_t e1 = lut[c1 * 16 + (s8 >> 4)];
+            const uint32_t mA = (cur.mA[S].a >> (8 * j)) & 0xFFu, mB = (cur.mA[S].b >> (8 * j)) & 0xFFu;
+            const uint32_t wnz = ((e0 >> 20) & 15u) | (((e1 >> 20) & 15u) << 4);
+            const bool slow = ((mA & (mB | wnz)) != 0u) | (p + 8 > cur.B) | (sp_nibeq(word, 15u) != 0u);
+            if (slow) {
+                mode = 9;
+            } else {
+                sp_apply<M>(a, r, env, vote, st, e0, c0, s8 & 15u, 8 * j, p, sid);
+                sp_apply<M>(a, r, env, vote, st, e1, c1, s8 >> 4, 8 * j + 4, p + 4, sid);
+                cur.ci += (uint32_t)__builtin_popcount(mA);
+                cur.pos = p + 8;
+            }
+        }
     }
-    if ((mc.h >= 0xF000u) & (mode != 3)) {  // a tie longer than the packed fields hold (never at 1 year)
+    if ((st.h >= 0xF000u) & (mode == 0)) {  // a tie longer than the hand-over's 16-bit fields (never at 1 year)
         cur.err |= SERR_SP;
         mode = 3;
     }
-    if (mode == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cur.A[j] = cur.N[j];
-        cur.mA = cur.mN;
-        sp_chunk_at(a, r, c + 2, cur.N, cur.mN);
-    }
+    if (mode == 0) sp_chunk_at(a, r, c + SP_PF, cur.A[S], cur.mA[S]);
     return mode;
 }
 
@@ -410,11 +645,14 @@ struct SpSrc {
 // A lane leaves the nibble form for the engine: mode 1 (its candidate at cur.pos needs the engine: the FIFO is
 // seeded from the candidate's list entry, found through the segment's slots) or mode 4 (it reached B with
 // T_B < D: the FIFO is seeded by redrawing B's super-group from its record). The settled state is handed to the
-// engine (msim_selm.h to_exact). Returns the new mode (2: engine, 3: error in cur.err). src: SpSrc.
+// engine (msim_selm.h to_exact) with the honest branch's composition counted from the nibbles of [prs, pos) and
+// the engine-handed blocks (C_A). Returns the new mode (2: engine, 3: error in cur.err). src: SpSrc.
 template <int M, class Src, class SelT, class Env>
-MSIM_HD int sp_enter(const SpArgs &a, uint32_t r, int mode, SpCur &cur, SelMacro<M> &mc, Src &src, SelT &s, Env &env,
+MSIM_HD int sp_enter(const SpArgs &a, uint32_t r, int mode, SpCur &cur, SpSt &st, Src &src, SelT &s, Env &env,
                      uint32_t m, const uint32_t *sids)
 {
+    const uint32_t sid = sids[0];
+    SelMacro<M> mc;
     auto &fifo = src.f;
     if (mode == 1) {
         const uint32_t idx = a.slots[((size_t)cur.sg * a.cap + cur.ci) * a.nr + r];
@@ -434,7 +672,7 @@ MSIM_HD int sp_enter(const SpArgs &a, uint32_t r, int mode, SpCur &cur, SelMacro
         const GroupRec gr = a.grec[(size_t)cur.gE * a.nr + r];
         fifo.d.ri = gr.ri;
         fifo.d.rp = gr.rp;
-        uint32_t I = gr.w0 >> 5, k = gr.w0 & 31u;  // the group's first block
+        uint32_t I = gr.w0 >> 5, k = gr.w0 & 31u;  // the super-group's first block
         uint32_t kB = k;
         for (uint32_t b = sp_sg_block(a, cur.gE); b <= cur.B; ++b) {  // draws up to block B + 1
             kB = k;
@@ -453,14 +691,119 @@ MSIM_HD int sp_enter(const SpArgs &a, uint32_t r, int mode, SpCur &cur, SelMacro
     fifo.n = 1;
     fifo.fill();
     src.pk = mc.k;
+    // the settled state, its honest branch as per-miner counts
+    mc.F = st.F;
+    mc.h = st.h;
+    mc.w = st.w;
+    mc.sst = st.sst;
+    mc.Ff = st.F;
+#pragma unroll
+    for (int i = 0; i < SelMacro<M>::NP; ++i) mc.pend[i] = mc.stp[i] = 0;
+    if (st.pxf) {
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            if ((uint32_t)j != sid) SelMacro<M>::field_add(mc.pend, SelMacro<M>::slot((uint32_t)j, sid), env.get(C_A, (uint32_t)j));
+    }
+    // the honest blocks of [prs, pos), a word at a time (the words' loads issued together)
+    for (uint32_t w0 = st.prs >> 3; w0 * 8 < cur.pos; w0 += 4) {
+        uint32_t wd[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) wd[q] = (w0 + q) * 8 < cur.pos ? a.nib[sp_nib_index(a.nr, r, w0 + q)] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t p = (w0 + q) * 8;
+            if (p >= cur.pos) continue;
+            const uint32_t lo = st.prs > p ? st.prs - p : 0u, hi = cur.pos - p < 8u ? cur.pos - p : 8u;
+            const uint32_t in = sp_bits(lo, hi);  // blocks of the word inside the range
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+                if ((uint32_t)j == sid) continue;
+                const uint32_t z = sp_nibeq(wd[q], (uint32_t)j);
+                const uint32_t n = (uint32_t)__builtin_popcount((sp_pack4(z) | (sp_pack4(z >> 16) << 4)) & in);
+                if (n) SelMacro<M>::field_add(mc.pend, SelMacro<M>::slot((uint32_t)j, sid), n);
+            }
+        }
+    }
+    st.sst = 0;
     mc.to_exact(env, s, m, sids);
     return 2;
 }
 
-// A lane in the engine steps it (msim_sel.h step) until the run is over (finish) or the engine hands the run
-// back to the settled form below B (msim_selm.h take_back: the nibble form resumes at the source's pending
-// block, sp_seek); past B the engine keeps the run to its end (only the last ~prop_k + prop_s of a run is
-// there). The kernel writes this step inline (msim_sel_kernels.hip msim_selpipe_kernel, and the host driver in
+// The engine hands the run back to the nibble form at block pidx (msim_selm.h take_back gave tb): the fork's
+// honest branch composition waits in C_A (take_back left the deep counters zero) and the range restarts at pidx.
+template <int M, class Env>
+MSIM_HD void sp_handback(Env &env, const SelMacro<M> &tb, SpSt &st, uint32_t pidx, uint32_t sid)
+{
+    st.F = tb.F;
+    st.h = tb.h;
+    st.w = tb.w;
+    st.sst = tb.sst;
+    uint32_t any = 0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t v = (uint32_t)j == sid ? 0u : tb.pend_of((uint32_t)j, sid);
+        env.set(C_A, (uint32_t)j, v);
+        any |= v;
+    }
+    st.pxf = any ? 1u : 0u;
+    st.prs = pidx;
+}
+
+// main.cpp:185-189 from a settled state (msim_selm.h SelMacro::finish): the honest branch is the best chain
+// (first seen), the selfish tie and withheld blocks are not in it.
+template <int M, class Env>
+MSIM_HD void sp_finish(Env &env, const SpSt &st, uint32_t sid, SelOut &out)
+{
+    if (st.sst) {
+        env.add(C_S, sid, st.sst);
+        env.add(C_F, sid, 0u - st.sst);
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        out.found[j] = env.get(C_F, (uint32_t)j) - ((uint32_t)j == sid ? st.h + st.w : 0u);
+        out.stale[j] = env.get(C_S, (uint32_t)j);
+    }
+    out.best_height = st.F + st.h;
+    out.err = 0;
+}
+
+// The run's honest stale blocks of the nibble form, per miner: the stale masks of chunks [0, st.schunk) from
+// SpArgs::stale and st.smask for the current chunk, against the chunks' finder nibbles (end of the run).
+// Eight chunks' loads in flight per batch (it runs once per run, at its end).
+template <int M>
+MSIM_HD void sp_stale_counts(const SpArgs &a, uint32_t r, const SpSt &st, uint32_t sid, uint32_t (&cnt)[M])
+{
+#pragma unroll
+    for (int j = 0; j < M; ++j) cnt[j] = 0;
+    for (uint32_t c0 = 0; c0 <= st.schunk; c0 += 8) {
+        uint32_t sm[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t c = c0 + i;
+            sm[i] = c < st.schunk ? a.stale[(size_t)c * a.nr + r] : (c == st.schunk ? st.smask : 0u);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            if (!sm[i]) continue;
+            uint32_t w[4];
+            CMask m;
+            sp_chunk_at(a, r, c0 + i, w, m);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t b8 = (sm[i] >> (8 * q)) & 0xFFu;
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    if ((uint32_t)j == sid) continue;
+                    const uint32_t z = sp_nibeq(w[q], (uint32_t)j);
+                    cnt[j] += (uint32_t)__builtin_popcount((sp_pack4(z) | (sp_pack4(z >> 16) << 4)) & b8);
+                }
+            }
+        }
+    }
+}
+
+// The engine phase (msim_sel.h step until the run is over or the engine hands it back below B, msim_selm.h
+// take_back) is written inline in the kernel (msim_sel_kernels.hip msim_selpipe_kernel, and the host driver in
 // tests/native/selpipe_host.cpp): as a helper taking the finish record and the taken-back state by reference,
 // both stayed live across the engine step and the engine loop spilled ~3x more.
 

@@ -4,7 +4,7 @@
 # WRITE_SIZE / instruction mix) and the c3 E1 stall split.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-TAG=${TAG:-final} PROF=1 bash scripts/gpu_rehearsal.sh || exit 1
+TAG=${TAG:-final} PROF=1 bash scripts/archive/gpu_rehearsal.sh || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-final}/pmc; mkdir -p $O
 P="python3 bench.py --config c2 --steps 1 --warmup 0 --streams 1 --no-cpu-baseline"

@@ -3,7 +3,7 @@
 #   pytest -m gpu (unless NOTEST=1), smoke (SMOKE=1), the default bench line with the CPU baseline (unless
 #   NOBENCH=1), and for every config in CFGS (default c2 c3 c5) rocprofv3 --kernel-trace --stats summaries of
 #   the exact bench commands, default two streams (_s0) and --streams 1 (_s1), then (PMC=1) the counter passes
-#   behind the bench line's PMC constants (scripts/gpu_pmc.sh). Output under gpurun_out/$TAG.
+#   behind the bench line's PMC constants (scripts/gpu_pmc_r05.sh). Output under gpurun_out/$TAG.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

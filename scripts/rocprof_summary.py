@@ -53,5 +53,17 @@ def main(path: str) -> None:
         print(f"| `{short}` | {calls} | {tot / 1e6:.3f} | {avg / 1e6:.4f} | {pct:.2f} | {bz:.4f} |")
 
 
+def calls(path: str, substr: str) -> None:
+    """Per-dispatch durations (us) of the kernels whose name contains substr, in dispatch order."""
+    db = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)[0]
+    c = sqlite3.connect(db)
+    rows = [(n, a, b) for n, a, b in c.execute("select name, start, end from kernels order by start") if substr in n]
+    for i, (n, a, b) in enumerate(rows):
+        print(f"{i} {(b - a) / 1e3:.1f} {n.split('(')[0][:60]}")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if len(sys.argv) > 3 and sys.argv[2] == "--calls":
+        calls(sys.argv[1], sys.argv[3])
+    else:
+        main(sys.argv[1])

@@ -108,7 +108,7 @@ struct EnvRef {  // SpSrc's found-counter access on the host: the lane's one Hos
 };
 
 struct Stats {
-    uint64_t words, enters, draw_enters, errors;
+    uint64_t words, enters, draw_enters, errors, slow;
 };
 Stats g_st;
 
@@ -189,6 +189,11 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
     a.list = list.data();
     a.nib = nib.data();
     a.cmask = cmask.data();
+    std::vector<uint32_t> stalev((size_t)L.nb / 32 * n, 0u);
+    a.stale = stalev.data();
+    uint32_t lut[SP_LUT];
+    for (int i = 0; i < SP_LUT; ++i) lut[i] = sp_lut_entry((uint32_t)i / 16u, (uint32_t)i % 16u);
+    auto vote = [](bool b) { return b; };
     uint64_t cum[MAXM];
     uint64_t c = 0;
     uint32_t sids[SEL_MAXS] = {SEL_NONE, SEL_NONE, SEL_NONE, SEL_NONE};
@@ -210,9 +215,8 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
         drw.cum = cum;
         drw.m = M;
         sp_begin(a, r, D, thr, drw, cur);
-        SelMacro<M> mc;
-        mc.F = mc.h = mc.w = mc.sst = mc.Ff = 0;
-        for (int i = 0; i < SelMacro<M>::NP; ++i) mc.pend[i] = mc.stp[i] = 0;
+        SpSt st;
+        st.F = st.h = st.w = st.sst = st.prs = st.pxf = st.smask = st.schunk = st.hbits = 0;
         Sel<M, 1, 1, 4, 1, 4> s;
         SpSrc<Fifo, EnvRef> src;
         src.f.d.cum = cum;
@@ -225,37 +229,58 @@ int run_sp(const uint64_t *perc, const int64_t *prop, const uint8_t *self, int64
         SelOut out;
         memset(&out, 0, sizeof(out));
         int mode = cur.err ? 3 : 0;
-        while (mode != 3) {
+        uint32_t ring = 0;
+        while (mode != 3) {  // as msim_selpipe_kernel, one lane
             if (mode == 0) {
                 ++g_st.words;
-                mode = sp_chunk<M>(a, r, env, [](bool b) { return b; }, cur, mc, sid, D);
+                // ring slot: table steps since the last refill, mod SP_PF (as the kernel's unrolled steps)
+                switch (ring++ % SP_PF) {
+                case 0: mode = sp_chunk<M, 0>(a, r, env, vote, lut, cur, st, sid); break;
+                case 1: mode = sp_chunk<M, 1 % SP_PF>(a, r, env, vote, lut, cur, st, sid); break;
+                case 2: mode = sp_chunk<M, 2 % SP_PF>(a, r, env, vote, lut, cur, st, sid); break;
+                default: mode = sp_chunk<M, 3 % SP_PF>(a, r, env, vote, lut, cur, st, sid); break;
+                }
+            } else if (mode == 9) {
+                ++g_st.slow;
+                mode = sp_slow_word<M>(a, r, env, cur, st, sid, D);
+                if (mode == 0) {
+                    sp_refill(a, r, cur);
+                    ring = 0;
+                }
             } else if (mode == 6) {
-                mc.finish(env, sid, out);
+                sp_finish<M>(env, st, sid, out);
                 mode = 3;
             } else if (mode == 1 || mode == 4) {
                 ++(mode == 1 ? g_st.enters : g_st.draw_enters);
-                mode = sp_enter<M>(a, r, mode, cur, mc, src, s, env, (uint32_t)M, sids);
-            } else {  // the engine (as msim_selpipe_kernel's engine loop)
+                mode = sp_enter<M>(a, r, mode, cur, st, src, s, env, (uint32_t)M, sids);
+            } else {  // the engine
                 if (!s.step(env, src, D)) {
                     s.finish(env, D, out);
                     mode = 3;
                 } else if (src.pidx < src.B) {
                     SelMacro<M> tb;
                     if (tb.take_back(env, s, sid)) {
-                        mc = tb;
+                        sp_handback<M>(env, tb, st, src.pidx, sid);
                         sp_seek(a, r, cur, src.pidx);
-                        mode = cur.err ? 3 : 0;
+                        mode = (cur.pos & 7u) ? sp_slow_word<M>(a, r, env, cur, st, sid, D) : 0;
+                        if (mode == 0) {
+                    sp_refill(a, r, cur);
+                    ring = 0;
+                }
                     }
                 }
             }
         }
         uint32_t e = cur.err | out.err;
         if (e) ++g_st.errors;
-        uint32_t F[M];
-        if (!e) sp_counts<M>(a, r, cur, F);
+        uint32_t F[M], X[M];
+        if (!e) {
+            sp_counts<M>(a, r, cur, F);
+            sp_stale_counts<M>(a, r, st, sid, X);
+        }
         for (int k = 0; k < M; ++k) {
-            found[(size_t)r * M + k] = e ? 0 : out.found[k] + F[k];
-            stale[(size_t)r * M + k] = e ? 0 : out.stale[k];
+            found[(size_t)r * M + k] = e ? 0 : out.found[k] + F[k] - X[k];
+            stale[(size_t)r * M + k] = e ? 0 : out.stale[k] + X[k];
         }
         best_h[r] = e ? 0 : out.best_height;
         err[r] = e;
@@ -271,7 +296,8 @@ extern "C" void selpipe_stats(uint64_t *out)
     out[1] = g_st.enters;
     out[2] = g_st.draw_enters;
     out[3] = g_st.errors;
-    g_st = Stats{0, 0, 0, 0};
+    out[4] = g_st.slow;
+    g_st = Stats{0, 0, 0, 0, 0};
 }
 
 // perc (integer percentages summing to 100), prop, selfish (exactly one), m miners. Per run: found/stale [n][m],

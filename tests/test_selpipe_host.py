@@ -36,7 +36,7 @@ def sp(native_tests):
                              (ctypes.c_uint8 * m)(*[1 if x else 0 for x in selfish]), m, duration, seed_base,
                              run_begin, n, cap, slots, p(f), p(s), p(bh), p(err))
         assert rc == 0, rc
-        st = (ctypes.c_uint64 * 4)()
+        st = (ctypes.c_uint64 * 5)()
         lib.selpipe_stats(st)
         return f.astype(np.int64), s.astype(np.int64), bh, err, list(st)
 
