@@ -210,7 +210,8 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #define SEL_MC_LDS 1  // the settled-form state waits in LDS during engine phases
 #endif
 template <int M, class SelT, class Env, class Src>
-__device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P, int64_t D, SelOut &o, uint32_t *mcs)
+__device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P, int64_t D, SelOut &o, uint32_t *mcs,
+                                          const uint32_t *lut)
 {
     SelMacro<M> mc;
     // A lane that finishes parks its counters in its own LDS counter rows (C_F, C_S) so that no result
@@ -227,6 +228,9 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
     };
     const uint32_t sid = P->sids[0];
     const int64_t ps = P->prop[sid];
+    int64_t thrmax = 0;  // the largest settle threshold of an honest find (SelMacro::step4)
+    for (uint32_t j = 0; j < P->m; ++j)
+        if (j != sid) thrmax = P->prop[j] + ps > thrmax ? P->prop[j] + ps : thrmax;
     const bool mac = P->macro != 0u;  // wave-uniform (one point per workgroup)
     const int xth = (int)__builtin_amdgcn_readfirstlane(P->xth >= 1u && P->xth <= 64u ? P->xth : (uint32_t)SEL_XTH);
     int mode = 0;
@@ -308,12 +312,12 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
 #endif
         } else {
             for (;;) {
-                // SEL_MSTEPS settled-form steps per exit test (a lane that leaves the form skips the rest)
+                // SEL_MSTEPS settled-form steps (four finds each when none needs the engine) per exit test (a
+                // lane that leaves the form skips the rest)
 #pragma unroll
                 for (int u = 0; u < SEL_MSTEPS; ++u) {
                     if (mode == 0) {
-                        src.prefetch();  // consumed at a later refill (peek settles only when it must)
-                        const int r = mc.step(env, src, D, sid, ps);
+                        const int r = mc.step4(env, src, D, sid, ps, thrmax, lut);
                         if (r == 2) {
                             SelOut q;
                             mc.finish(env, sid, q);
@@ -377,10 +381,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
     __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
+    __shared__ uint32_t s_tab[SP_LUT];  // four-find transitions (msim_selm.h sp_lut_entry)
     __shared__ int64_t s_prop[MAXM];
     __shared__ uint8_t s_lut[128];
     __shared__ LogTab s_log[1];
     const uint32_t tid = threadIdx.x;
+    if (tid < SP_LUT) s_tab[tid] = sp_lut_entry(tid / 16u, tid % 16u);
     const uint32_t wps = (a.sn + TPB - 1) / TPB;
     const uint32_t point = a.plist[blockIdx.x / wps], blk = blockIdx.x % wps;
     const SelParams *P = a.pts + point;
@@ -418,7 +424,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         if (a.force_retry) {
             o.err = SERR_CAP;
         } else if constexpr (NS == 1) {
-            sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid]);
+            sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid], s_tab);
         } else {  // several selfish miners: the engine alone
             Sel<M, NS, NA, NG, NQ, NC> s;
             s.init(P->m, P->sids);
@@ -723,9 +729,12 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
     __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
+    __shared__ uint32_t s_tab[SP_LUT];  // four-find transitions (msim_selm.h sp_lut_entry)
     const uint32_t tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
+    if (tid < SP_LUT) s_tab[tid] = sp_lut_entry(tid / 16u, tid % 16u);
+    __syncthreads();
     const uint32_t c = *a.counts, lim = c < a.err_cap ? c : a.err_cap;
     const uint32_t idx = blockIdx.x * TPB + tid;
     if (idx >= lim) return;
@@ -741,7 +750,7 @@ __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
     src.n = 0;
     SelOut o;
     if constexpr (NS == 1) {  // the mixed schedule, with the engine's wide capacities
-        sel_mixed<M, Sel<M, NS, 4, 16, 4, SEL_NC>>(env, src, P, P->duration_ms, o, &s_mc[0][tid]);
+        sel_mixed<M, Sel<M, NS, 4, 16, 4, SEL_NC>>(env, src, P, P->duration_ms, o, &s_mc[0][tid], s_tab);
     } else {
         Sel<M, NS, 4, 16, 4, SEL_NC> s;
         s.init(P->m, P->sids);

@@ -34,15 +34,60 @@
 
 namespace msim {
 
-// A FIFO of up to three held draws in front of a drawer that makes the reference's draws in-lane
-// (void D::draw(uint32_t &interval_ms, uint32_t &finder)). In the settled form it holds two draws at the
-// start of every step and spec() adds the third from streams that advance whatever the step's outcome, so
-// the draw arithmetic has no dependency on the transition it runs beside; a lane that leaves the form
-// keeps all three for the engine, which takes them first (next/peek), then draws on demand.
+// The settled-form transitions (msim_selm.h SelMacro::transition) of four blocks with selfish pattern s4 (bit i:
+// block i is the selfish miner's; the others honest) from lead class cls (w = cls; cls 6 stands for any
+// w >= 6, from which no resolution can happen within four blocks), as one 27-bit table entry:
+//   bits 0-3   w after the four blocks (cls 6: the change + 4)
+//   bit 4      some resolution (honest find at w == 0: the honest branch wins; at w == 2: the selfish one)
+//   bit 5      the first resolution is a selfish win (the honest branch open before the half is stale)
+//   bits 6-8   ties since the last resolution (none: since the half's start)
+//   bits 9-12  F's increase beyond the entering h (which the first resolution adds)
+//   bits 13-15 selfish stale blocks beyond the entering h (which a first resolution by an honest win adds)
+//   bits 16-19 honest blocks of the half made stale by selfish wins
+//   bits 20-23 w != 0 before block i (a candidate there needs the engine)
+//   bits 24-26 one past the last resolution's block (0: none)
+MSIM_HD uint32_t sp_lut_entry(uint32_t cls, uint32_t s4)
+{
+    uint32_t w = cls, hrel = 0, rs = 0, fsw = 0, dF = 0, dsst = 0, st = 0, wnz = 0, lrs = 0, rstart = 0;
+    for (uint32_t i = 0; i < 4; ++i) {
+        if (w != 0) wnz |= 1u << i;
+        if ((s4 >> i) & 1u) {
+            w += 1;
+            continue;
+        }
+        if (w == 0 || w == 2) {
+            const bool res = w == 0;
+            dF += hrel + (res ? 1u : 2u);
+            if (res) dsst += hrel;
+            else
+                for (uint32_t j = rstart; j <= i; ++j)
+                    if (!((s4 >> j) & 1u)) st |= 1u << j;
+            if (!rs) fsw = res ? 0u : 1u;
+            rs = 1;
+            hrel = 0;
+            w = 0;
+            rstart = i + 1;
+            lrs = i + 1;
+        } else {
+            hrel += 1;
+            w -= 1;
+        }
+    }
+    const uint32_t wf = cls < 6 ? w : w + 4u - 6u;
+    return wf | (rs << 4) | (fsw << 5) | (hrel << 6) | (dF << 9) | (dsst << 13) | (st << 16) | (wnz << 20) | (lrs << 24);
+}
+constexpr int SP_LUT = 7 * 16;
+
+// A FIFO of up to four held draws in front of a drawer that makes the reference's draws in-lane
+// (void D::draw(uint32_t &interval_ms, uint32_t &finder)). The settled form's four-find step (step4) tops it up
+// to four; the one-find step holds two at its start and spec() adds the third from streams that advance
+// whatever the step's outcome, so the draw arithmetic has no dependency on the transition it runs beside. A
+// lane that leaves the form keeps its held draws for the engine, which takes them first (next/peek), then
+// draws on demand.
 template <class D>
 struct SelFifo {
     D d;
-    uint32_t I0, k0, I1, k1, I2, k2;
+    uint32_t I0, k0, I1, k1, I2, k2, I3, k3;
     uint32_t n;  // held draws
     MSIM_HD bool peek(uint32_t &I, uint32_t &k)
     {
@@ -60,6 +105,8 @@ struct SelFifo {
         k0 = k1;
         I1 = I2;
         k1 = k2;
+        I2 = I3;
+        k2 = k3;
         n -= 1u;
     }
     MSIM_HD void pop_if(bool p)
@@ -68,7 +115,16 @@ struct SelFifo {
         k0 = p ? k1 : k0;
         I1 = p ? I2 : I1;
         k1 = p ? k2 : k1;
+        I2 = p ? I3 : I2;
+        k2 = p ? k3 : k2;
         n -= p ? 1u : 0u;
+    }
+    // step4: four held draws (from at least two)
+    MSIM_HD void top4()
+    {
+        if (n < 3u) d.draw(I2, k2);
+        if (n < 4u) d.draw(I3, k3);
+        n = 4u;
     }
     MSIM_HD bool next(uint32_t &I, uint32_t &k)
     {
@@ -233,6 +289,81 @@ struct SelMacro {
         T += ok ? (int64_t)I : 0;
         k = ok ? kn : k;
         return ok ? (T < D ? 0 : 2) : 1;
+    }
+
+    // One find from held draws only (the FIFO holds at least one): step() without the speculative draw.
+    template <class Env, class Src>
+    MSIM_HD int step1(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
+    {
+        const int64_t pk = env.prop_tab(k < (uint32_t)M ? k : 0u);
+        uint32_t I = 0, kn = 0;
+        src.peek(I, kn);
+        const bool is_s = k == sid;
+        const int64_t thr = is_s ? 0 : pk + (w != 0u ? ps : 0);
+        const bool ok = (k < (uint32_t)M) & (h < 0xFFFFu) & (F - Ff < 0xFF00u) & (is_s | (((int64_t)I > thr) & (T + thr < D)));
+        transition(k, is_s, ok, sid);
+        env.add(C_F, k < (uint32_t)M ? k : 0u, ok ? 1u : 0u);
+        src.pop_if(ok);
+        T += ok ? (int64_t)I : 0;
+        k = ok ? kn : k;
+        return ok ? (T < D ? 0 : 2) : 1;
+    }
+
+    // Four finds at once when none of them can need the engine: the pending find and the next three, from four
+    // held draws (src: SelFifo; topped up here). The transitions come from the four-block table (lut:
+    // sp_lut_entry, SP_LUT entries) indexed by the lead class and the selfish pattern; the honest branch's
+    // composition follows the table's resolution points. A find needs the engine iff it is honest and
+    // I_next <= prop_k + (w != 0 ? prop_s : 0) (step), i.e. B (I_next <= prop_k) or A (<= prop_k + prop_s) with
+    // w != 0, which the table's "w != 0 before block i" bits decide for all four; the settle times are all
+    // below D when the fourth find's plus the largest threshold (thrmax) is. Otherwise one find by step1.
+    // Returns as step().
+    template <class Env, class Src>
+    MSIM_HD int step4(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps, int64_t thrmax, const uint32_t *lut)
+    {
+        src.top4();
+        const uint32_t kk[4] = {k, src.k0, src.k1, src.k2};
+        const uint32_t In[4] = {src.I0, src.I1, src.I2, src.I3};
+        uint32_t s4 = 0, a4 = 0, b4 = 0;
+        bool valid = true;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            valid &= kk[j] < (uint32_t)M;
+            const bool is_s = kk[j] == sid;
+            const int64_t pk = env.prop_tab(kk[j] < (uint32_t)M ? kk[j] : 0u);
+            s4 |= (is_s ? 1u : 0u) << j;
+            a4 |= ((!is_s) & ((int64_t)In[j] <= pk + ps) ? 1u : 0u) << j;
+            b4 |= ((!is_s) & ((int64_t)In[j] <= pk) ? 1u : 0u) << j;
+        }
+        const int64_t T3 = T + (int64_t)In[0] + (int64_t)In[1] + (int64_t)In[2];
+        const uint32_t cls = w < 6u ? w : 6u;
+        const uint32_t e = lut[cls * 16 + s4];
+        const bool fast = valid & ((b4 | (a4 & ((e >> 20) & 15u))) == 0u) & (T3 + thrmax < D) & (h < 0xFFF0u) &
+                          (F - Ff < 0xFEF0u);
+        if (!fast) return step1(env, src, D, sid, ps);
+        const uint32_t rs = (e >> 4) & 1u, fsw = (e >> 5) & 1u, hl = (e >> 6) & 7u, st4 = (e >> 16) & 15u,
+                       lrs = (e >> 24) & 7u;
+        F += (rs ? h : 0u) + ((e >> 9) & 15u);
+        sst += ((rs & (fsw ^ 1u)) ? h : 0u) + ((e >> 13) & 7u);
+        h = rs ? hl : h + hl;
+        w = cls == 6u ? w + (e & 15u) - 4u : (e & 15u);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            stp[i] += fsw ? pend[i] : 0ull;
+            pend[i] = rs ? 0ull : pend[i];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool hon = ((s4 >> j) & 1u) == 0u;
+            const uint32_t sl = slot(kk[j], sid);
+            field_add(stp, sl, (hon & (((st4 >> j) & 1u) != 0u)) ? 1u : 0u);  // made stale by a selfish win
+            field_add(pend, sl, (hon & ((uint32_t)j >= lrs)) ? 1u : 0u);      // the honest branch after the last resolution
+            env.add(C_F, kk[j], 1u);
+        }
+        T = T3 + (int64_t)In[3];
+        k = src.k3;
+        src.n = 0u;
+        src.fill();
+        return T < D ? 0 : 2;
     }
 
     template <class Env>

@@ -380,49 +380,6 @@ MSIM_HD void sp_counts(const SpArgs &a, uint32_t r, const SpCur &c, uint32_t (&F
 
 
 // ---------------------------------------------------------------- the settled form over nibbles
-// The settled-form transitions (msim_selm.h SelMacro::transition) of four blocks with selfish pattern s4 (bit i:
-// block i is the selfish miner's; the others honest) from lead class cls (w = cls; cls 6 stands for any
-// w >= 6, from which no resolution can happen within four blocks), as one 27-bit table entry:
-//   bits 0-3   w after the four blocks (cls 6: the change + 4)
-//   bit 4      some resolution (honest find at w == 0: the honest branch wins; at w == 2: the selfish one)
-//   bit 5      the first resolution is a selfish win (the honest branch open before the half is stale)
-//   bits 6-8   ties since the last resolution (none: since the half's start)
-//   bits 9-12  F's increase beyond the entering h (which the first resolution adds)
-//   bits 13-15 selfish stale blocks beyond the entering h (which a first resolution by an honest win adds)
-//   bits 16-19 honest blocks of the half made stale by selfish wins
-//   bits 20-23 w != 0 before block i (a candidate there needs the engine)
-//   bits 24-26 one past the last resolution's block (0: none)
-MSIM_HD uint32_t sp_lut_entry(uint32_t cls, uint32_t s4)
-{
-    uint32_t w = cls, hrel = 0, rs = 0, fsw = 0, dF = 0, dsst = 0, st = 0, wnz = 0, lrs = 0, rstart = 0;
-    for (uint32_t i = 0; i < 4; ++i) {
-        if (w != 0) wnz |= 1u << i;
-        if ((s4 >> i) & 1u) {
-            w += 1;
-            continue;
-        }
-        if (w == 0 || w == 2) {
-            const bool res = w == 0;
-            dF += hrel + (res ? 1u : 2u);
-            if (res) dsst += hrel;
-            else
-                for (uint32_t j = rstart; j <= i; ++j)
-                    if (!((s4 >> j) & 1u)) st |= 1u << j;
-            if (!rs) fsw = res ? 0u : 1u;
-            rs = 1;
-            hrel = 0;
-            w = 0;
-            rstart = i + 1;
-            lrs = i + 1;
-        } else {
-            hrel += 1;
-            w -= 1;
-        }
-    }
-    const uint32_t wf = cls < 6 ? w : w + 4u - 6u;
-    return wf | (rs << 4) | (fsw << 5) | (hrel << 6) | (dF << 9) | (dsst << 13) | (st << 16) | (wnz << 20) | (lrs << 24);
-}
-constexpr int SP_LUT = 7 * 16;
 
 // The form moves to chunk c: the stale mask of the chunk it leaves is stored (SpArgs::stale starts zeroed, so
 // chunks with no stale block, and chunks the engine consumed, are never written).

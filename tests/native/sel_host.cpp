@@ -78,6 +78,15 @@ struct MixStats {
     uint64_t macro_steps, exact_steps, entries;
 };
 MixStats g_mix;
+struct LutInit {  // the four-find table (msim_selm.h sp_lut_entry), as the kernels keep it in LDS
+    uint32_t t[SP_LUT];
+    LutInit()
+    {
+        for (int i = 0; i < SP_LUT; ++i) t[i] = sp_lut_entry((uint32_t)i / 16u, (uint32_t)i % 16u);
+    }
+};
+const LutInit g_lut_init;
+const uint32_t *g_lut = g_lut_init.t;
 
 template <int M, int NS, int NA, int NG, int NQ, int NC>
 void run_mixed(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t D, SelOut &o)
@@ -91,6 +100,9 @@ void run_mixed(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t 
     SelMacro<M> mc;
     s.init((uint32_t)M, sids);
     const uint32_t sid = sids[0];
+    int64_t thrmax = 0;  // as msim_sel_kernels.hip sel_mixed
+    for (int j = 0; j < M; ++j)
+        if ((uint32_t)j != sid) thrmax = prop[j] + prop[sid] > thrmax ? prop[j] + prop[sid] : thrmax;
     if (!mc.begin(src)) {
         o.err = SERR_DRAWS;
         return;
@@ -103,7 +115,7 @@ void run_mixed(const int64_t *prop, const uint32_t *sids, HostSrc &src, int64_t 
     for (;;) {
         if (macro) {
             ++g_mix.macro_steps;
-            const int r = mc.step(env, src, D, sid, prop[sid]);
+            const int r = mc.step4(env, src, D, sid, prop[sid], thrmax, g_lut);
             if (r == 2) {
                 mc.finish(env, sid, o);
                 return;

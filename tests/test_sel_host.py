@@ -268,7 +268,8 @@ def test_mixed_full_year(sel, oracle, native_tests, h, prop):
     for r in range(2):
         _check(sel, oracle, percs, [prop] * 9, [True] + [False] * 8, D, 1000 + 2 * r, 1001 + 2 * r, caps=10)
     macro, exact, entries = _mix_stats(native_tests)
-    assert macro > 2 * exact and entries > 0
+    # a settled-form step carries up to four finds (SelMacro::step4), an engine step one event
+    assert 4 * macro > 2 * exact and entries > 0
 
 
 def test_mixed_edge_cases(sel, oracle):
