@@ -24,7 +24,7 @@ for c in ${CFGS-c2 c3 c5}; do
   for s in ${STREAMS:-0 1}; do
     B=""; [ $s = 1 ] && B="--streams 1"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_${c}_s$s -o prof -- python3 bench.py --config $c $B --no-cpu-baseline > $O/bench_${c}_s$s.json 2> $O/prof_${c}_s$s.err || { tail -20 $O/prof_${c}_s$s.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/bench_${c}_s$s.json'));r=d['roofline'];print('$c s$s',d['value'],d['ms_per_step'],r.get('frac'),r['dominant_ms'],r['dominant_span_ms'])"
+    python3 -c "import json;d=json.load(open('$O/bench_${c}_s$s.json'));r=d['roofline'];print('$c s$s',d['value'],d['ms_per_step'],r.get('frac'),r['dominant_ms'],r['kernels_busy_ms'])"
     python3 scripts/rocprof_summary.py $O/prof_${c}_s$s > $O/rocprof_${c}_s$s.md
     head -6 $O/rocprof_${c}_s$s.md
     rm -rf $O/prof_${c}_s$s

@@ -20,6 +20,6 @@ for c in ${CFGS-c3 c2 c1}; do
     else
       timeout -k 10 300 python3 bench.py --config $c $B --no-cpu-baseline ${BENCH_ARGS} > $O/bench_${c}_s$st.json 2> $O/bench_${c}_s$st.err || { tail -20 $O/bench_${c}_s$st.err; exit 1; }
     fi
-    python3 -c "import json;d=json.load(open('$O/bench_${c}_s$st.json'));r=d['roofline'];print('$c s$st',d['value'],d['ms_per_step'],r.get('frac'),r['dominant_ms'],r['kernel_ms'])"
+    python3 -c "import json;d=json.load(open('$O/bench_${c}_s$st.json'));r=d['roofline'];print('$c s$st',d['value'],d['ms_per_step'],r.get('frac'),r['dominant_ms'],r['kernels_busy_ms'])"
   done
 done

@@ -51,6 +51,8 @@ def test_single_rank_unchanged():
     # no time in the roofline exceeds the step (the dominant kernel's busy time is a share of the step)
     roof = d["roofline"]
     assert roof["dominant_ms"] <= d["ms_per_step"] + 1e-9
+    assert roof["kernels_busy_ms"] <= d["ms_per_step"] + 1e-9
+    assert not any(k.endswith("span_ms") for k in roof)
 
 
 def test_spawn_eight_ranks():
