@@ -1,5 +1,6 @@
-"""The entity-engine path (msim_sel.h; D1 word draws -> E1 engine -> E2 retries) on the GPU, through the
-C ABI, against the oracle and the reference's own published results.
+"""The entity-engine path on the GPU (E1: the settled form msim_selm.h with in-lane draws and engine phases of
+msim_sel.h -> E2 retries -> G), through the C ABI, against the oracle and the reference's own published
+results.
 
 Bit-exact per-run counters where the oracle can follow; at BASELINE sizes, size-independent properties
 (sum of found = best height, no failed run, E1 == E2) and the reference's README results (README.md:56-63,
@@ -80,8 +81,9 @@ def test_gpu_weighted_selfish_vs_oracle(msim, oracle):
 
 @pytest.mark.parametrize("h,prop", [(40, 1000), (49, 30_000), (10, 100), (25, 10_000)])
 def test_gpu_engine_equals_retry_kernel(msim, monkeypatch, h, prop):
-    """E1 (words from D1, fast capacities) and E2 (draws recomputed in-lane from the seeds, wide
-    capacities) are two device paths through the engine: 2048 runs, identical per-run counters."""
+    """E1 (in-lane fast draws, the settled form's four-find steps, fast engine capacities) and E2 (exact draws
+    recomputed from the seeds, wide capacities) are two device paths through the engine: 2048 runs, identical
+    per-run counters."""
     miners = msim.setup_miners(prop, selfish_perc=h)
     a = msim.Simulation(miners).run(2048, 31_000, 1000, 0, per_run=True)
     monkeypatch.setenv("MSIM_SEL_FORCE_RETRY", "1")
