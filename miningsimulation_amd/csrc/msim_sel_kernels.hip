@@ -78,22 +78,13 @@ struct SelExactDraw {
         I = (uint32_t)next_interval(ri);
         k = sel_pick_weighted<M>(rng_next(rp), P);
     }
-    uint32_t pI, pk;
-    __device__ void draw_spec_a() { draw(pI, pk); }
-    __device__ void draw_spec_b(uint32_t &I, uint32_t &k)
-    {
-        I = pI;
-        k = pk;
-    }
-    __device__ void fix(uint32_t &, uint32_t &) {}
 };
 
 // Fast sequence (E1 without a word stream): K1's table interval with its exactness check and exact
 // fallback (msim_fastdraw.h), the finder through the LDS code table for percentages (W = 100) or the
-// weighted scan otherwise (wave-uniform choice). The settled form's speculative draw is split in two:
-// draw_spec() is branch-free (fast interval, fast table pick, the two exactness flags, both uniforms kept)
-// so that the compiler can interleave it with the transition it runs beside, and fix() — at the end of
-// the step — redoes what the fast forms cannot settle (rare; every pick of a weighted network).
+// weighted scan otherwise (wave-uniform choice). The fast forms are branch-free (fast interval, fast table
+// pick, the two exactness flags) so that the compiler can interleave a draw with the transitions it runs
+// beside; the branch at the end redoes what they cannot settle (rare; every pick of a weighted network).
 template <int M>
 struct SelFastDraw {
     Rng ri, rp;
@@ -102,62 +93,43 @@ struct SelFastDraw {
     const SelParams *P;
     FdConsts kc;
     bool wt;
-    // the speculative draw between its parts: both uniforms (until fix()), the interval's reduced argument,
-    // exponent and table entries (until draw_spec_b()), the pick's acceptance key and finder
-    uint64_t su_i, su_p;
-    double sw, sinvc, sA;
-    int32_t se;
-    uint32_t skp, sk;
-    bool sx_i, sx_p;      // the interval / pick need the exact forms
-    // part A: both RNG steps, the table indices and the LDS reads (log table, finder table)
-    __device__ __forceinline__ void draw_spec_a()
+    __device__ __forceinline__ void draw(uint32_t &I, uint32_t &k)
     {
-        su_i = rng_next(ri);
-        su_p = rng_next(rp);
-        const uint32_t lo = (uint32_t)su_i, hi = (uint32_t)(su_i >> 32);
+        // both RNG steps, the table indices and the LDS reads (log table, finder table)
+        const uint64_t u_i = rng_next(ri);
+        const uint64_t u_p = rng_next(rp);
+        const uint32_t lo = (uint32_t)u_i, hi = (uint32_t)(u_i >> 32);
         const double c = __builtin_fma(u32_to_f64(lo >> 11), -0x1.0p-53, 1.0);
         const double v = __builtin_fma(u32_to_f64(hi), -0x1.0p-32, c);  // 1 - (u>>11) 2^-53, exact
         const uint64_t vb = __builtin_bit_cast(uint64_t, v);
         const uint32_t vh = (uint32_t)(vb >> 32);
-        se = (int)(vh >> 20) - 1023;
+        const int32_t e = (int)(vh >> 20) - 1023;
         const uint32_t j = (vh >> (20 - LOG_BITS)) & (LOG_TAB - 1);
-        sw = __builtin_bit_cast(double, (vb & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+        const double w = __builtin_bit_cast(double, (vb & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
         uint32_t aoff = j * 8u;
         asm("" : "+v"(aoff));
-        sA = *(const double *)((const char *)lt->A + aoff);
-        sinvc = lt->invc[j];
-        sk = lut[pick_q_fast_key(su_p, skp)];  // q = 100: PickFinder falls through (finder >= m)
-    }
-    // part B: the interval polynomial (msim_fastdraw.h interval_fast_z, the same operations) and the flags
-    __device__ __forceinline__ void draw_spec_b(uint32_t &I, uint32_t &k)
-    {
-        const double r = __builtin_fma(sw, sinvc, -1.0);
+        const double A = *(const double *)((const char *)lt->A + aoff);
+        const double invc = lt->invc[j];
+        uint32_t kp;
+        k = lut[pick_q_fast_key(u_p, kp)];  // q = 100: PickFinder falls through (finder >= m)
+        // the interval polynomial (msim_fastdraw.h interval_fast_z, the same operations) and the flags
+        const double r = __builtin_fma(w, invc, -1.0);
         double p = __builtin_fma(r, kc.c5, kc.c4);
         p = __builtin_fma(r, p, kc.c3);
         p = __builtin_fma(r, p, kc.c2);
         p = __builtin_fma(r, p, kc.c1);
-        const double z0 = __builtin_fma(r, p, sA);
-        const double z = __builtin_fma((double)se, FD_CE, z0);
+        const double z0 = __builtin_fma(r, p, A);
+        const double z = __builtin_fma((double)e, FD_CE, z0);
         I = (uint32_t)(int32_t)z;
         const double f = __builtin_amdgcn_fract(z);
         const uint32_t ki = (uint32_t)(__builtin_bit_cast(uint64_t, f) >> 32) - FD_OK_LO;
-        k = sk;
-        sx_i = ki >= FD_OK_RANGE;
-        sx_p = skp >= PICK_RARE_LO;
-    }
-    __device__ __forceinline__ void fix(uint32_t &I, uint32_t &k)
-    {
-        if (sx_i | sx_p | wt) {
-            if (sx_i) I = (uint32_t)interval_ms_exact_dev(su_i);
-            if (wt) k = sel_pick_weighted<M>(su_p, P);
-            else if (sx_p) k = lut[pick_q_exact(su_p)];
+        const bool x_i = ki >= FD_OK_RANGE;
+        const bool x_p = kp >= PICK_RARE_LO;
+        if (x_i | x_p | wt) {
+            if (x_i) I = (uint32_t)interval_ms_exact_dev(u_i);
+            if (wt) k = sel_pick_weighted<M>(u_p, P);
+            else if (x_p) k = lut[pick_q_exact(u_p)];
         }
-    }
-    __device__ __forceinline__ void draw(uint32_t &I, uint32_t &k)
-    {
-        draw_spec_a();
-        draw_spec_b(I, k);
-        fix(I, k);
     }
 };
 

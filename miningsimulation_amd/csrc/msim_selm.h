@@ -80,8 +80,8 @@ constexpr int SP_LUT = 7 * 16;
 
 // A FIFO of up to four held draws in front of a drawer that makes the reference's draws in-lane
 // (void D::draw(uint32_t &interval_ms, uint32_t &finder)). The settled form's four-find step (step4) tops it up
-// to four; the one-find step holds two at its start and spec() adds the third from streams that advance
-// whatever the step's outcome, so the draw arithmetic has no dependency on the transition it runs beside. A
+// to four (draws from streams that advance whatever the steps' outcomes, so the draw arithmetic has no
+// dependency on the transitions it runs beside); the one-find step (step1) takes a held draw. A
 // lane that leaves the form keeps its held draws for the engine, which takes them first (next/peek), then
 // draws on demand.
 template <class D>
@@ -132,16 +132,6 @@ struct SelFifo {
         pop();
         return true;
     }
-    // The settled form's speculative draw in three parts, so that the compiler can overlap the draw's table
-    // reads and arithmetic with the transition it runs beside: spec() (RNG steps, table reads; n == 2 here,
-    // fill() on every entry into the form), spec_b() (arithmetic) and spec_fix() (the rare exact forms).
-    MSIM_HD void spec()
-    {
-        d.draw_spec_a();
-        n = 3u;
-    }
-    MSIM_HD void spec_b() { d.draw_spec_b(I2, k2); }
-    MSIM_HD void spec_fix() { d.fix(I2, k2); }
     MSIM_HD void fill()
     {
         if (n == 0u) {
@@ -265,33 +255,11 @@ struct SelMacro {
         for (int i = 0; i < NP; ++i) pend[i] = rs ? 0ull : pend[i];
     }
 
-    // One find. Returns 0 (next find pending), 1 (this find needs the entity engine), 2 (run over: the
-    // next find is at or after D). src.spec() lets a source that draws in-lane produce a later draw that
-    // does not depend on this step's outcome, so its arithmetic overlaps the transition below.
-    template <class Env, class Src>
-    MSIM_HD int step(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
-    {
-        const int64_t pk = env.prop_tab(k < (uint32_t)M ? k : 0u);  // read before the draw's table reads
-        src.spec();
-        uint32_t I = 0, kn = 0;
-        const bool have = src.peek(I, kn);
-        const bool is_s = k == sid;
-        const int64_t thr = is_s ? 0 : pk + (w != 0u ? ps : 0);
-        // (F - Ff bounds the honest stale blocks added to stp since the last flush: a lane about to reach
-        // 2^16 takes the engine path, whose hand-over flushes)
-        const bool ok = have & (k < (uint32_t)M) & (h < 0xFFFFu) & (F - Ff < 0xFF00u) &
-                        (is_s | (((int64_t)I > thr) & (T + thr < D)));
-        transition(k, is_s, ok, sid);
-        env.add(C_F, k < (uint32_t)M ? k : 0u, ok ? 1u : 0u);
-        src.spec_b();  // the speculative draw is completed in I2 / k2 before pop_if can shift it
-        src.spec_fix();
-        src.pop_if(ok);
-        T += ok ? (int64_t)I : 0;
-        k = ok ? kn : k;
-        return ok ? (T < D ? 0 : 2) : 1;
-    }
-
-    // One find from held draws only (the FIFO holds at least one): step() without the speculative draw.
+    // One find from held draws (the FIFO holds at least one). Returns 0 (next find pending), 1 (this find
+    // needs the entity engine), 2 (run over: the next find is at or after D). A find needs the engine when
+    // it is honest and the next interval does not clear its propagation threshold (prop_k, plus prop_s while
+    // the selfish miner leads), or when a 16-bit field could overflow (h, or the honest stale blocks added to
+    // stp since the last flush, bounded by F - Ff: the engine's hand-over flushes).
     template <class Env, class Src>
     MSIM_HD int step1(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps)
     {
@@ -316,7 +284,7 @@ struct SelMacro {
     // I_next <= prop_k + (w != 0 ? prop_s : 0) (step), i.e. B (I_next <= prop_k) or A (<= prop_k + prop_s) with
     // w != 0, which the table's "w != 0 before block i" bits decide for all four; the settle times are all
     // below D when the fourth find's plus the largest threshold (thrmax) is. Otherwise one find by step1.
-    // Returns as step().
+    // Returns as step1().
     template <class Env, class Src>
     MSIM_HD int step4(Env &env, Src &src, int64_t D, uint32_t sid, int64_t ps, int64_t thrmax, const uint32_t *lut)
     {

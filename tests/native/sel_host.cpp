@@ -48,14 +48,6 @@ struct HostDraw {
         while ((int)f < m && cum[f] <= q) ++f;
         k = f;  // == m: fell through (simulation.h:220)
     }
-    uint32_t pI = 0, pk = 0;
-    void draw_spec_a() { draw(pI, pk); }
-    void draw_spec_b(uint32_t &I, uint32_t &k)
-    {
-        I = pI;
-        k = pk;
-    }
-    void fix(uint32_t &, uint32_t &) {}
 };
 using HostSrc = SelFifo<HostDraw>;
 

@@ -92,14 +92,6 @@ struct HostDraw {
         while ((int)f < m && cum[f] <= q) ++f;
         k = f;
     }
-    uint32_t pI = 0, pk = 0;
-    void draw_spec_a() { draw(pI, pk); }
-    void draw_spec_b(uint32_t &I, uint32_t &k)
-    {
-        I = pI;
-        k = pk;
-    }
-    void fix(uint32_t &, uint32_t &) {}
 };
 using Fifo = SelFifo<HostDraw>;
 struct EnvRef {  // SpSrc's found-counter access on the host: the lane's one HostEnv
