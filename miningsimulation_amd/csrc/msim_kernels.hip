@@ -158,8 +158,8 @@ __global__ __launch_bounds__(TPB, 2) void msim_sweep_kernel(const SimParams *__r
 __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
 
 // K2: one lane per listed non-fast block (msim_pipeline.h episode_entry).
-// Three resident waves per SIMD (168 VGPRs): the lean state machine fits them without spills; four waves
-// (128 VGPRs) spill and run slower (136.6 vs 79.6 us, profiles/r04/k2v2).
+// The lean state machine at three resident waves per SIMD (168 VGPRs; k2_waves below); four waves (128 VGPRs)
+// spill and run slower (136.6 vs 79.6 us, profiles/r04/k2v2).
 #ifndef MSIM_K2_WAVES
 #define MSIM_K2_WAVES 3
 #endif
@@ -173,10 +173,15 @@ __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int3
 #endif
 constexpr int K2_TPB = MSIM_K2_TPB, K3_TPB = MSIM_K3_TPB;
 static_assert(K3_TPB % 64 == 0 && K3_TPB <= TPB && TPB % K3_TPB == 0, "K3 workgroups: whole waves, dividing TPB");
+// Resident K2 waves per SIMD by (miner count, kind). The lean machine takes three waves (168 VGPRs) up to 9 miners:
+// at 9 it spills 5 VGPRs there and is still faster than at two waves without spills (78.0 vs 86.3 us per c2
+// launch, profiles/r05/k2waves); from 10 miners it spills 21-554 at three waves and takes two (one at 15). The mid
+// machine needs 259 VGPRs from 14 miners and takes one wave there. Every other instantiation has no VGPR spills.
+constexpr int k2_waves(int m, int kind) { return kind == 0 ? (m <= 9 ? MSIM_K2_WAVES : m <= 14 ? 2 : 1) : (m <= 13 ? 2 : 1); }
 // The mid and full state machines at two waves per SIMD (256 VGPRs): at three (168) the mid one spilled 31
 // VGPRs, the full one 132; a rho > 0.002 network lists ~10x the lean one's blocks, so K2 still fills the chip.
 template <int M, int KIND>
-__global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(KIND == 0 ? MSIM_K2_WAVES : 2, 8))) void msim_episode_kernel(const SimParams p,
+__global__ __launch_bounds__(K2_TPB) __attribute__((amdgpu_waves_per_eu(k2_waves(M, KIND), 8))) void msim_episode_kernel(const SimParams p,
                                                                                                     const PipeArgs a)
 {
     // the draw tables in LDS: an episode's draws read them in its dependent chain (global: ~600-900 cycles

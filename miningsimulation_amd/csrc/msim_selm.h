@@ -299,8 +299,8 @@ struct SelMacro {
             const bool is_s = kk[j] == sid;
             const int64_t pk = env.prop_tab(kk[j] < (uint32_t)M ? kk[j] : 0u);
             s4 |= (is_s ? 1u : 0u) << j;
-            a4 |= ((!is_s) & ((int64_t)In[j] <= pk + ps) ? 1u : 0u) << j;
-            b4 |= ((!is_s) & ((int64_t)In[j] <= pk) ? 1u : 0u) << j;
+            a4 |= (((!is_s) & ((int64_t)In[j] <= pk + ps)) ? 1u : 0u) << j;
+            b4 |= (((!is_s) & ((int64_t)In[j] <= pk)) ? 1u : 0u) << j;
         }
         const int64_t T3 = T + (int64_t)In[0] + (int64_t)In[1] + (int64_t)In[2];
         const uint32_t cls = w < 6u ? w : 6u;
