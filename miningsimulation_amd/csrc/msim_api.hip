@@ -1250,6 +1250,22 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
                 }
             if (!placed) w->groups.push_back({nc, {i}});
         }
+        // A group's workgroups are dispatched in point-list order, and a point's runs cost in proportion to its
+        // engine entries: an honest find needs the engine when the next interval is below prop_k (+ prop_s while
+        // the selfish miner leads). The costliest points go first, so the launch ends on cheap workgroups
+        // (longest-first list scheduling); results are indexed by point, not by list position.
+        auto cost = [&](uint32_t p) {
+            const msim::SelParams &s = w->sps[p];
+            if (!s.macro) return 1e30;  // the engine for every find
+            const int64_t ps = s.prop[s.sids[0]];
+            double c = 0.0;
+            for (uint32_t k = 0; k < s.m; ++k)
+                if (k != s.sids[0]) c += (double)(s.cum[k] - (k ? s.cum[k - 1] : 0)) * (double)(s.prop[k] + ps);
+            return c / (double)s.W;
+        };
+        if (!getenv("MSIM_SWEEP_LISTED_ORDER"))  // A/B: the caller's point order
+            for (auto &g : w->groups)
+                std::stable_sort(g.points.begin(), g.points.end(), [&](uint32_t a, uint32_t b) { return cost(a) > cost(b); });
     }
     *out = w;
     return MSIM_OK;
