@@ -191,9 +191,11 @@ struct DevCtx {
 
 // Resident K1 waves per SIMD the register budget is sized for (VGPRs <= 512 / waves). Measured on MI355X
 // (c2, profiles/r03/INDEX.md): 4 waves (113 VGPRs) 4.17 ms, 5 (96) 4.02 ms, 6 (80) 3.75 ms, 7 (72) 7.3 ms and
-// 8 (64) 13.7 ms, where the spills reach the draw loop's hot values.
+// 8 (64) 13.7 ms, where the spills reach the draw loop's hot values. Re-measured on round 5's K1 (chunked list
+// reservation; profiles/r05/k1waves): 4 waves (104 VGPRs) 3.27 ms, 5 (96, 10 spills) 3.17-3.21 ms, 6 (80, 23
+// spills) 3.27 ms serial, same box, alternating.
 #ifndef MSIM_K1_WAVES
-#define MSIM_K1_WAVES 6
+#define MSIM_K1_WAVES 5
 #endif
 // NIB: the selfish pipeline's K1 (msim_selpipe.h): every block's finder nibble stored, a block listed when
 // I_{i+1} < fthr (STRICT; its table gives honest finders fthr = prop_k + prop_s + 1, selfish ones 0).

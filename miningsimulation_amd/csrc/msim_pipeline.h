@@ -364,8 +364,8 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
 #else
             const FdConsts kq = kc;
 #endif
-            // The quad's start states are read only on the two rare paths below; at K1's 80-VGPR budget (6
-            // waves per SIMD, msim_drawgen.hip) the compiler keeps them in scratch, written once per quad.
+            // The quad's start states are read only on the two rare paths below; at K1's register budget (96
+            // VGPRs at 5 waves per SIMD, msim_drawgen.hip) the compiler keeps them in scratch, written once per quad.
             // Measured on MI355X: recovering them by inverse stepping instead (no scratch, 84 VGPRs) made K1
             // 11 % slower at the same occupancy (profiles/r03/INDEX.md, k1 A/B).
             const Rng ri0 = ri, rp0 = rp;
