@@ -34,7 +34,8 @@ extern "C" {
 #define MSIM_E_SELFISH (-3)  /* reserved (round 2 rejected selfish networks the entity engine cannot serve;
                                 every network with selfish miners now runs, those on the general engine) */
 #define MSIM_E_MINERS (-4)   /* network too large for the general engine: one run's explicit chains (miners x
-                                blocks a run can have x 12 B) would exceed 8 GiB of device memory */
+                                blocks a run can have x 12 B) would exceed 96 GiB (msim_config_create), or the
+                                launch's workspace exceeds the device's free memory (msim_run, msim_sweep_run) */
 #define MSIM_E_HIP (-5)      /* HIP runtime error (no device, launch failure, out of memory) */
 #define MSIM_E_CAPACITY (-6) /* a run outgrew every window of the general engine (its last window holds every
                                 block a run of the config's duration can have: practically never) */

@@ -89,7 +89,8 @@ struct msim_config {
     // wide combine cannot hold.
     GenHost gh;
     bool general = false;
-    bool selfish = false;  // some miner is selfish (G's window tiers, msim_general_launch.h gen_tiers)
+    bool selfish = false;   // some miner is selfish
+    bool gen_full = false;  // G keeps its full last window tier (msim_general_launch.h gen_needs_full)
     std::vector<std::pair<int, void *>> gtables;  // per device: GenParams + arrays
 };
 
@@ -113,6 +114,7 @@ struct msim_sweep {
     std::vector<std::pair<int, void *>> sdev;  // (device, SelParams[n_points] + point lists)
     // General-engine view of every point (G finishes what E2 cannot; a sweep with a general point runs on G)
     bool general = false;
+    bool gen_full = false;  // some point needs G's full last window tier (gen_needs_full)
     std::vector<GenHost> gens;
     std::vector<std::pair<int, void *>> gdev;  // (device, GenParams[n_points] + arrays)
 };
@@ -762,7 +764,10 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     const bool gen = nself > (uint32_t)msim::SEL_MAXS || (nself && n > MSIM_MAX_MINERS) || id_quirk ||
                      n > msim::WIDE_MAX_M || getenv("MSIM_FORCE_GENERAL") != nullptr;
     // G holds every miner's explicit chain: one lane of its last window must fit (msim_general_launch.h).
-    if (gen && !msim::gen_fits(n, duration_ms, nself > 0)) return MSIM_E_MINERS;
+    int64_t max_prop = 0;
+    for (uint32_t k = 0; k < n; ++k) max_prop = miners[k].propagation_ms > max_prop ? miners[k].propagation_ms : max_prop;
+    const bool gen_full = msim::gen_needs_full(nself > 0, max_prop);
+    if (gen && !msim::gen_fits(n, duration_ms, gen_full)) return MSIM_E_MINERS;
     const bool sel = nself > 0 && !gen;
     const bool narrow = n <= MSIM_MAX_MINERS && (total_weight == 100 || sel);
     const bool force_wide = getenv("MSIM_FORCE_WIDE") != nullptr && nself == 0;
@@ -772,6 +777,7 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
     c->total_weight = total_weight;
     c->general = gen;
     c->selfish = nself > 0;
+    c->gen_full = gen_full;
     c->gh.duration_ms = duration_ms;
     c->gh.W = total_weight;
     for (uint32_t k = 0; k < n; ++k) {
@@ -918,7 +924,7 @@ uint32_t msim_config_miner_count(const msim_config *cfg) { return cfg ? cfg->n :
 size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
 {
     if (!cfg || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return 0;
-    if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->selfish).total;
+    if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->gen_full).total;
     if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
     if (cfg->sel)
         return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total + (cfg->sp_ok ? sp_layout(cfg, n_runs).total : 0);
@@ -933,7 +939,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
 {
     if (!cfg || !d_sums || !d_status || !d_workspace || n_runs == 0 || n_runs > MAX_LAUNCH_RUNS) return MSIM_E_INVALID;
     if (cfg->general) {
-        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->selfish);
+        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->gen_full);
         if (workspace_bytes < w.total) return MSIM_E_INVALID;
         msim_config *c = const_cast<msim_config *>(cfg);
         const msim::GenParams *gp = nullptr;
@@ -1127,6 +1133,14 @@ void msim_sums_to_stats(const msim_sums *sums, uint32_t n, msim_stats *out)
     }
 }
 
+// Whether a workspace of `bytes` fits the current device's free memory (hipMemGetInfo).
+static bool workspace_fits(size_t bytes)
+{
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return true;  // let the allocation report it
+    return bytes <= fr;
+}
+
 int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32_t seed_base, int device,
              msim_stats *out_sums, msim_sums *opt_sums, msim_run_record *opt_per_run, uint32_t *opt_best_height)
 {
@@ -1145,6 +1159,9 @@ int msim_run(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uint32
     std::vector<uint64_t> acc(6 * (size_t)m, 0), part(6 * (size_t)m);
     uint32_t st[2];
     hipStream_t s = nullptr;
+    // G's last window can need tens of GB for one lane of a large network (msim_general_launch.h): a
+    // workspace larger than the device's free memory is the network's size limit, not a HIP failure
+    if (cfg->general && !workspace_fits(wsb)) return MSIM_E_MINERS;
     if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&sums, 6 * sizeof(uint64_t) * m) != hipSuccess ||
         hipMalloc(&status, 2 * sizeof(uint32_t)) != hipSuccess ||
         (want_rec && hipMalloc(&rec, chunk * m * sizeof(msim_run_record)) != hipSuccess) ||
@@ -1222,6 +1239,7 @@ int msim_sweep_create(const msim_config *const *cfgs, uint32_t n_points, msim_sw
         w->self = w->self || cfgs[i]->selfish || cfgs[i]->p.selfish >= 0;
         w->sel = w->sel || cfgs[i]->sel;
         w->general = w->general || cfgs[i]->general;
+        w->gen_full = w->gen_full || cfgs[i]->gen_full;
         w->gens.push_back(cfgs[i]->gh);
         w->max_duration = cfgs[i]->p.duration_ms > w->max_duration ? cfgs[i]->p.duration_ms : w->max_duration;
     }
@@ -1286,7 +1304,7 @@ uint32_t msim_sweep_miner_count(const msim_sweep *sw) { return sw ? sw->m : 0u; 
 size_t msim_sweep_workspace_bytes(const msim_sweep *sw, uint64_t runs_per_point)
 {
     if (!sw || runs_per_point == 0 || runs_per_point * sw->pts.size() > MAX_LAUNCH_RUNS) return 0;
-    if (sw->general) return gen_only_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration, sw->self).total;
+    if (sw->general) return gen_only_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration, sw->gen_full).total;
     if (sw->sel) return sel_ws_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point, sw->max_duration).total;
     return sweep_layout(sw->m, (uint32_t)sw->pts.size(), runs_per_point).total;
 }
@@ -1306,7 +1324,7 @@ int msim_sweep_launch(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_pe
         const int rc = gen_cached(sm->mu, sm->gdev, hs, &gp);
         if (rc) return rc;
         if (sw->general) {
-            const GenOnlyWs w = gen_only_layout(sw->m, np, runs_per_point, sw->max_duration, sw->self);
+            const GenOnlyWs w = gen_only_layout(sw->m, np, runs_per_point, sw->max_duration, sw->gen_full);
             if (workspace_bytes < w.total) return MSIM_E_INVALID;
             return gen_launch_impl(sw->m, np, gp, w, (char *)d_workspace, run_begin, runs_per_point, seed_base, d_sums,
                                    d_per_run, d_best_height, d_status, (hipStream_t)stream);
@@ -1411,6 +1429,7 @@ int msim_sweep_run(const msim_sweep *sw, uint64_t run_begin, uint64_t runs_per_p
     uint32_t st[2] = {0, 0};
     hipStream_t s = nullptr;
     int rc = MSIM_OK;
+    if (sw->general && !workspace_fits(wsb)) return MSIM_E_MINERS;  // as in msim_run
     if (hipMalloc(&ws, wsb) != hipSuccess || hipMalloc(&sums, hs.size() * sizeof(msim_sums)) != hipSuccess ||
         hipMalloc(&status, sizeof(st)) != hipSuccess ||
         (opt_per_run && hipMalloc(&rec, nr * m * sizeof(msim_run_record)) != hipSuccess) ||
@@ -1480,32 +1499,49 @@ int msim_timing_read_stages(double *draws_ms, double *engine_ms, double *launch_
     return rc;
 }
 
-// Union length of (begin, end) event pairs: every event timed against the first begin (same device), the
-// intervals sorted and merged.
+// Union length of (begin, end) event pairs. Events are timed against an anchor of their own device: a pair
+// whose begin cannot be timed against an existing anchor (hipEventElapsedTime fails across devices) starts a
+// new group with its begin as the anchor. Each group's intervals are sorted and merged; the result is the
+// largest group's busy time (one device's), so a timed run over several devices reads instead of failing.
 static int busy_ms(const std::vector<hipEvent_t> &v, double *out)
 {
     *out = 0;
     if (v.size() < 2) return MSIM_OK;
-    std::vector<std::pair<double, double>> iv;
+    std::vector<hipEvent_t> anchors;
+    std::vector<std::vector<std::pair<double, double>>> groups;
     for (size_t i = 0; i + 1 < v.size(); i += 2) {
-        float a = 0, b = 0;
-        if (hipEventSynchronize(v[i + 1]) != hipSuccess || hipEventElapsedTime(&a, v[0], v[i]) != hipSuccess ||
-            hipEventElapsedTime(&b, v[0], v[i + 1]) != hipSuccess)
-            return MSIM_E_HIP;
-        iv.emplace_back(a, b);
-    }
-    std::sort(iv.begin(), iv.end());
-    double lo = iv[0].first, hi = iv[0].second, acc = 0;
-    for (const auto &p : iv) {
-        if (p.first > hi) {
-            acc += hi - lo;
-            lo = p.first;
-            hi = p.second;
-        } else if (p.second > hi) {
-            hi = p.second;
+        if (hipEventSynchronize(v[i + 1]) != hipSuccess) return MSIM_E_HIP;
+        bool placed = false;
+        for (size_t g = 0; g < anchors.size() && !placed; ++g) {
+            float a = 0, b = 0;
+            if (hipEventElapsedTime(&a, anchors[g], v[i]) != hipSuccess) continue;
+            if (hipEventElapsedTime(&b, anchors[g], v[i + 1]) != hipSuccess) return MSIM_E_HIP;
+            groups[g].emplace_back(a, b);
+            placed = true;
+        }
+        if (!placed) {
+            float b = 0;
+            if (hipEventElapsedTime(&b, v[i], v[i + 1]) != hipSuccess) return MSIM_E_HIP;
+            anchors.push_back(v[i]);
+            groups.push_back({{0.0, (double)b}});
         }
     }
-    *out = acc + (hi - lo);
+    (void)hipGetLastError();  // the failed cross-device queries leave an error behind
+    for (auto &iv : groups) {
+        std::sort(iv.begin(), iv.end());
+        double lo = iv[0].first, hi = iv[0].second, acc = 0;
+        for (const auto &p : iv) {
+            if (p.first > hi) {
+                acc += hi - lo;
+                lo = p.first;
+                hi = p.second;
+            } else if (p.second > hi) {
+                hi = p.second;
+            }
+        }
+        acc += hi - lo;
+        *out = acc > *out ? acc : *out;
+    }
     return MSIM_OK;
 }
 
@@ -1538,7 +1574,7 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     memset(out, 0, sizeof(*out));
     out->rho = cfg->rho;
     if (cfg->general) {
-        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->selfish);
+        const GenOnlyWs w = gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->gen_full);
         out->uses_pipeline = 4;
         out->slice_runs = (uint32_t)w.g.tier[0].lanes;
         out->segment_blocks = w.g.tier[0].cap;
@@ -1682,7 +1718,7 @@ const char *msim_strerror(int code)
     case MSIM_E_INVALID: return "invalid argument";
     case MSIM_E_WEIGHTS: return "miner weights must be integers adding up to the total weight (100 for percentages)";
     case MSIM_E_SELFISH: return "reserved (not returned: every network with selfish miners runs)";
-    case MSIM_E_MINERS: return "network too large for the general engine (one run's explicit chains, miners x blocks per run x 12 B, exceed 8 GiB)";
+    case MSIM_E_MINERS: return "network too large for the general engine (one run's explicit chains, miners x blocks per run x 12 B, exceed 96 GiB, or the launch's workspace exceeds the device's free memory)";
     case MSIM_E_HIP: return "HIP runtime error";
     case MSIM_E_CAPACITY: return "a run exceeded the compact state capacity";
     case MSIM_E_PICK: return "PickFinder fell through its table";

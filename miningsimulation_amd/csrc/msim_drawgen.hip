@@ -108,12 +108,16 @@ struct DevCtx {
     __device__ __forceinline__ uint32_t packed(uint32_t w) const { return cnt[2 * w][tid] | (cnt[2 * w + 1][tid] << 16); }
     // The wave's reserved chunk of the episode list, [lend - lleft, lend) still free (wave-uniform).
     uint32_t lend, lleft;
-    // Mark the unused tail of the wave's chunk (K2 skips EP_HOLE slots; no run's slots point there).
+    // Mark the unused tail of the wave's chunk (K2 skips EP_HOLE slots; no run's slots point there). A chunk
+    // holds up to max(lchunk, 64) slots, so the tail can be longer than the wave: every slot of it is marked,
+    // 64 per pass (K2 reads every slot below the list count, and the workspace is not cleared between launches).
     __device__ void holes()
     {
         uint32_t lane;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=&v"(lane));
-        if (lane < lleft && lend - lleft + lane < a.lcap) a.list[lend - lleft + lane].run = EP_HOLE;
+        const uint32_t lo = lend - lleft;
+        for (uint32_t i = lane; i < lleft; i += 64u)
+            if (lo + i < a.lcap) a.list[lo + i].run = EP_HOLE;
     }
     __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp,
                          uint32_t fthr)

@@ -3,7 +3,7 @@
 // G runs in up to three tiers of growing windows. Tier 1 takes its runs from a list (the runs the entity
 // engine's retry kernel E2 could not finish) or from an index range (networks only G serves: selfish miners
 // in networks of more than 15 miners, more than 4 selfish miners); a run whose chains outgrow the window is
-// appended to the next tier's list. The last tier's window holds every block a run can have.
+// appended to the next tier's list. The last tier's window holds every block a run can have (gen_tiers).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -46,14 +46,24 @@ struct GenTier {
 };
 
 // Window tiers for networks of up to max_m miners and runs of up to max_duration ms: 256 blocks (every
-// honest or minority-selfish run folds well inside it), 4 096, and, for networks with a selfish miner, the
-// largest chain a run can have (a selfish miner that never reveals: every block, mu + 10 sigma + 64). Honest
-// networks stop at 4 096: their forks fold far inside it, and a run that outgrew it anyway would fail with
-// MSIM_E_CAPACITY rather than reserve a window it never uses. Lanes per tier fill `budget` bytes: whole waves
+// honest or minority-selfish run folds well inside it), 4 096, and, when `full`, the largest chain a run can
+// have (mu + 10 sigma + 64 blocks: a selfish miner that never reveals holds every block). `full` is set for
+// networks with a selfish miner and for honest networks whose largest propagation delay could span a
+// quarter of the 4 096-block window (gen_needs_full): an honest fork folds once its blocks have arrived
+// everywhere, so the window needs about the blocks found within the largest delay. Any other honest network
+// stops at 4 096 and does not reserve a window it never uses. Lanes per tier fill `budget` bytes: whole waves
 // while a wave fits, down to ONE lane for a window too large for a wave (the last tier of a large selfish
 // network: a run only reaches it with a selfish majority, and a lane serves its list in turn).
-// One lane's chains may take up to a third of the MI355X's 288 GB of HBM; larger networks are rejected.
+// One lane's chains may take up to a third of the MI355X's 288 GB of HBM; larger networks are rejected at
+// config creation (MSIM_E_MINERS), and msim_run rejects a launch whose workspace exceeds the device's free
+// memory with the same code (msim_api.hip).
 constexpr double GEN_MAX_LANE_BYTES = 96.0 * 1024 * 1024 * 1024;
+inline bool gen_needs_full(bool selfish, int64_t max_prop_ms)
+{
+    if (selfish) return true;
+    const double mu = (double)max_prop_ms / 599999.5;
+    return mu + 10.0 * sqrt(mu > 1.0 ? mu : 1.0) + 64.0 >= 1024.0;
+}
 inline double gen_lane_bytes(uint32_t max_m, uint32_t cap) { return (double)max_m * (cap * 12.0 + 12.0); }
 inline uint32_t gen_last_cap(int64_t max_duration)
 {
@@ -62,10 +72,10 @@ inline uint32_t gen_last_cap(int64_t max_duration)
     top = (top + 255) / 256 * 256;
     return (uint32_t)(top > 4096 ? top : 4096);
 }
-inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTier (&t)[3], bool selfish)
+inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTier (&t)[3], bool full)
 {
     const uint32_t caps[3] = {256u, 4096u, gen_last_cap(max_duration)};
-    const int nt = selfish && caps[2] > 4096u ? 3 : 2;
+    const int nt = full && caps[2] > 4096u ? 3 : 2;
     for (int i = 0; i < nt; ++i) {
         double l = floor(budget / gen_lane_bytes(max_m, caps[i]));
         l = l >= 64.0 ? floor(l / 64.0) * 64.0 : (l >= 1.0 ? l : 1.0);
@@ -76,9 +86,9 @@ inline int gen_tiers(uint32_t max_m, int64_t max_duration, double budget, GenTie
     return nt;
 }
 // Whether G can hold a network of m miners and runs of duration_ms (one lane of its last window).
-inline bool gen_fits(uint32_t m, int64_t duration_ms, bool selfish)
+inline bool gen_fits(uint32_t m, int64_t duration_ms, bool full)
 {
-    return gen_lane_bytes(m, selfish ? gen_last_cap(duration_ms) : 4096u) <= GEN_MAX_LANE_BYTES;
+    return gen_lane_bytes(m, full ? gen_last_cap(duration_ms) : 4096u) <= GEN_MAX_LANE_BYTES;
 }
 
 // Workspace of G: the tier lists and the largest tier's chains and counters.
@@ -89,11 +99,11 @@ struct GenWs {
     size_t lists_off, sizes_off, owners_off, arrivals_off, total;
 };
 
-inline GenWs gen_ws_layout(uint32_t max_m, int64_t max_duration, uint32_t list_cap, double budget, bool selfish)
+inline GenWs gen_ws_layout(uint32_t max_m, int64_t max_duration, uint32_t list_cap, double budget, bool full)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     GenWs w;
-    w.nt = gen_tiers(max_m, max_duration, budget, w.tier, selfish);
+    w.nt = gen_tiers(max_m, max_duration, budget, w.tier, full);
     w.list_cap = list_cap;
     size_t lanes = 0, chain = 0;
     for (int i = 0; i < w.nt; ++i) {

@@ -5,8 +5,8 @@
 // thread (main.cpp:209-217). Runs are independent and their seeds are a pure function of the run index,
 // so here the run range is cut into contiguous shards, one per device; each device runs its shard
 // through msim_launch (device-resident, asynchronous on its own stream), and the per-miner msim_sums (integers)
-// are combined by ONE ncclAllReduce over a single-process communicator (ncclCommInitAll: RCCL over xGMI
-// on MI355X), cached per device list. Integer sums make the result bit-identical to msim_run for every
+// with the two status words packed behind them are combined by ONE ncclAllReduce per job over a single-process
+// communicator (ncclCommInitAll: RCCL over xGMI on MI355X), cached per device list. Integer sums make the result bit-identical to msim_run for every
 // device count.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -32,7 +32,8 @@ __global__ void add_sums_kernel(uint64_t *acc, const uint64_t *part, uint32_t n)
     if (i < n) acc[i] += part[i];
 }
 
-__global__ void add_status_kernel(uint32_t *acc, const uint32_t *part)
+// the launch's two status words, added as u64 behind the sums (one all-reduce operand)
+__global__ void add_status_kernel(uint64_t *acc, const uint32_t *part)
 {
     if (threadIdx.x < 2) acc[threadIdx.x] += part[threadIdx.x];
 }
@@ -45,8 +46,7 @@ struct Shard {
     int rc = MSIM_OK;
     hipStream_t s = nullptr;
     void *ws = nullptr;
-    uint64_t *d_acc = nullptr;   // [nv] sums of every chunk (the all-reduce operand)
-    uint32_t *d_stat = nullptr;  // [2] status of every chunk
+    uint64_t *d_acc = nullptr;   // [nv + 2] sums of every chunk, then their status words (the all-reduce operand)
     uint64_t *d_part = nullptr;  // [nv] one chunk's sums
     uint32_t *d_pst = nullptr;   // [2] one chunk's status
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // timing: shard start, shard done, all-reduce done
@@ -84,12 +84,10 @@ int alloc_shard(const Job &job, Shard &sh, bool timed)
     sh.wsb = sh.chunk ? job.ws_bytes(sh.chunk) : 0;
     if (sh.chunk && sh.wsb == 0) return MSIM_E_INVALID;
     if (hipSetDevice(sh.device) != hipSuccess || hipStreamCreate(&sh.s) != hipSuccess ||
-        hipMalloc(&sh.d_acc, nv * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&sh.d_stat, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&sh.d_acc, (nv + 2) * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&sh.d_part, nv * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&sh.d_pst, 2 * sizeof(uint32_t)) != hipSuccess || (sh.wsb && hipMalloc(&sh.ws, sh.wsb) != hipSuccess) ||
-        hipMemsetAsync(sh.d_acc, 0, nv * sizeof(uint64_t), sh.s) != hipSuccess ||
-        hipMemsetAsync(sh.d_stat, 0, 2 * sizeof(uint32_t), sh.s) != hipSuccess)
+        hipMemsetAsync(sh.d_acc, 0, (nv + 2) * sizeof(uint64_t), sh.s) != hipSuccess)
         return MSIM_E_HIP;
     if (timed)
         for (hipEvent_t &e : sh.ev)
@@ -104,7 +102,6 @@ void free_shard(Shard &sh)
     (void)hipFree(sh.d_part);
     (void)hipFree(sh.d_pst);
     (void)hipFree(sh.d_acc);
-    (void)hipFree(sh.d_stat);
     for (hipEvent_t &e : sh.ev)
         if (e) (void)hipEventDestroy(e);
     if (sh.s) (void)hipStreamDestroy(sh.s);
@@ -123,7 +120,7 @@ void enqueue_shard(const Job &job, uint32_t seed_base, Shard &sh)
         sh.rc = job.launch(sh.begin + off, cn, seed_base, sh.d_part, sh.d_pst, sh.ws, sh.wsb, sh.s);
         if (sh.rc) break;
         hipLaunchKernelGGL(add_sums_kernel, dim3((job.nv + 255) / 256), dim3(256), 0, sh.s, sh.d_acc, sh.d_part, job.nv);
-        hipLaunchKernelGGL(add_status_kernel, dim3(1), dim3(64), 0, sh.s, sh.d_stat, sh.d_pst);
+        hipLaunchKernelGGL(add_status_kernel, dim3(1), dim3(64), 0, sh.s, sh.d_acc + job.nv, sh.d_pst);
         if (hipGetLastError() != hipSuccess) sh.rc = MSIM_E_HIP;
     }
     if (sh.ev[1]) (void)hipEventRecord(sh.ev[1], sh.s);
@@ -187,9 +184,9 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
             rc = MSIM_E_HIP;
             coll_failed = true;
         } else if (ce.ok) {
-            for (uint32_t g = 0; g < n_devices; ++g)
-                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv, ncclUint64, ncclSum, ce.e->comms[g], sh[g].s) != ncclSuccess ||
-                    ncclAllReduce(sh[g].d_stat, sh[g].d_stat, 2, ncclUint32, ncclSum, ce.e->comms[g], sh[g].s) != ncclSuccess)
+            for (uint32_t g = 0; g < n_devices; ++g)  // sums and status: one collective per device
+                if (ncclAllReduce(sh[g].d_acc, sh[g].d_acc, job.nv + 2, ncclUint64, ncclSum, ce.e->comms[g], sh[g].s) !=
+                    ncclSuccess)
                     rc = MSIM_E_HIP;
             if (ncclGroupEnd() != ncclSuccess) rc = MSIM_E_HIP;
             coll_failed = rc != MSIM_OK;
@@ -214,16 +211,15 @@ int run_job(const Job &job, uint64_t run_begin, uint64_t n_runs, uint32_t seed_b
             opt_shard_ms[2 * g + 1] = b;
         }
     }
-    acc.assign(job.nv, 0);
-    uint32_t st[2] = {0, 0};
-    if (rc == MSIM_OK) {  // every device holds the reduced sums: read the first one's
+    acc.assign(job.nv + 2, 0);
+    if (rc == MSIM_OK) {  // every device holds the reduced sums and status: read the first one's
         if (hipSetDevice(sh[0].device) != hipSuccess ||
-            hipMemcpy(acc.data(), sh[0].d_acc, acc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(st, sh[0].d_stat, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess)
+            hipMemcpy(acc.data(), sh[0].d_acc, acc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
             rc = MSIM_E_HIP;
-        else if (st[1] != 0)
+        else if (acc[job.nv + 1] != 0)
             rc = MSIM_E_CAPACITY;
     }
+    acc.resize(job.nv);
     for (uint32_t g = 0; g < n_devices; ++g) free_shard(sh[g]);
     return rc;
 }

@@ -61,7 +61,8 @@ MAX_LAUNCH_RUNS = 1 << 26  # msim_launch's per-call limit (msim_api.hip); larger
 
 def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=None,
                 launch: Optional[Callable] = None, device=None, max_chunk: int = MAX_LAUNCH_RUNS):
-    """This rank's shard through msim_launch on the current device, then one all-reduce (RCCL on GPUs).
+    """This rank's shard through msim_launch on the current device, then one all-reduce (RCCL on GPUs) of the
+    sums with the status words packed behind them.
 
     Returns the global [M, 6] int64 sums as a tensor on `device` (identical on every rank). `launch`
     replaces sim.launch (same signature, workspace None) so that the partition, chunking, status check and
@@ -76,10 +77,12 @@ def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=No
     begin, n = shard(n_total, world, rank)
     m = len(sim.miners)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
-    status = torch.zeros(2, dtype=torch.int32, device=dev)
-    part = torch.zeros_like(sums)
-    pst = torch.zeros_like(status)
+    # the sums and the two status words in one buffer: ONE all-reduce per job
+    buf = torch.zeros(6 * m + 2, dtype=torch.int64, device=dev)
+    sums = buf[: 6 * m].view(m, 6)
+    status = buf[6 * m:]
+    part = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+    pst = torch.zeros(2, dtype=torch.int32, device=dev)
     chunk = min(n, max_chunk)
     ws = None
     if n and launch is None:
@@ -98,8 +101,7 @@ def run_sharded(sim, n_total: int, seed_base: int, run_begin: int = 0, stream=No
             sums += part
             status += pst
         if world > 1:
-            dist.all_reduce(sums)
-            dist.all_reduce(status)
+            dist.all_reduce(buf)
     if stream is not None and dev.type == "cuda":
         torch.cuda.current_stream(dev).wait_stream(stream)  # the caller's stream sees the result
     if int(status[1].item()) != 0:

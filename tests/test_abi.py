@@ -45,7 +45,6 @@ def test_config_validation_without_gpu(msim_lib_path):
     bad = [
         ([Miner(0, 60, 1000), Miner(1, 30, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 90
         ([Miner(0, 60, 1000), Miner(1, 50, 1000)], _lib.MSIM_E_WEIGHTS),            # sums to 110
-        # one run's explicit chains above 8 GiB on the general engine (20 000 miners x ~55 k blocks)
         # a selfish network whose one G lane (every block of every miner's chain) exceeds 96 GiB
         ([Miner(k, 1 if k < 100 else 0, 1000, k == 0) for k in range(160000)], _lib.MSIM_E_MINERS),
         ([Miner(0, 50, -1), Miner(1, 50, 1000)], _lib.MSIM_E_INVALID),
@@ -128,3 +127,22 @@ def test_report_format():
     out = report(miners, st, 32768).splitlines()
     assert out[0] == "After running 32768 simulations for 365d each, on average:"
     assert out[1] == "  - Miner 0 (30% of network hashrate) found 15621 blocks i.e. 30.0901% of blocks. Stale rate: 1.0092%."
+
+
+def test_general_engine_keeps_full_window_for_long_delays():
+    """G (msim_general_launch.h) drops its full-chain last window tier for honest networks, whose forks fold
+    within 4 096 blocks, but keeps it when the largest propagation delay could span a quarter of that window
+    (a honest network with delays of days would otherwise fail with MSIM_E_CAPACITY). Host-only:
+    msim_pipeline_info reports G's tier count as `segments`."""
+    from miningsimulation_amd import Miner, Simulation
+
+    def tiers(prop_ms, selfish=False):
+        miners = [Miner(k, 1 if k < 100 else 0, prop_ms, selfish and k == 0) for k in range(5000)]
+        info = Simulation(miners).pipeline_info(64)
+        assert info["uses_pipeline"] == 4, info
+        return info["segments"]
+
+    assert tiers(1000) == 2                 # 1 s: forks fold within a few blocks
+    assert tiers(6 * 3600 * 1000) == 2      # 6 h: ~36 blocks per delay
+    assert tiers(5 * 86400 * 1000) == 3     # 5 days: ~720 blocks per delay + 10 sigma + 64 > 1 024
+    assert tiers(1000, selfish=True) == 3   # a selfish miner can withhold every block

@@ -350,3 +350,34 @@ def test_gpu_overlapped_streams_equal_serial(msim, preset):
         assert int(status[1]) == 0
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("preset", ["c1", "c2"])
+def test_gpu_dirty_workspace_equals_clean(msim, preset):
+    """A launch must not depend on what its workspace held before (the driver's torch.empty buffers are
+    reused across launches). K1 reserves episode-list slots a wave chunk at a time and marks the unused tail
+    of every chunk; with c1's 10 s delays a chunk is 256 slots, longer than a wave, so the whole tail must be
+    marked. Filled with 0xFF bytes, the workspace's unmarked slots would send K2 to run and
+    segment indices far out of range."""
+    import torch
+
+    sim = msim.Simulation(msim.PRESETS[preset]())
+    m = len(sim.miners)
+    n = 8192
+    dev = torch.device("cuda", 0)
+    out = []
+    for fill in (0x00, 0xFF, 0x00):
+        ws = torch.full((sim.workspace_bytes(n),), fill, dtype=torch.uint8, device=dev)
+        sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+        status = torch.zeros(2, dtype=torch.int32, device=dev)
+        rec = torch.zeros((n, m, 2), dtype=torch.int32, device=dev)
+        bh = torch.zeros(n, dtype=torch.int32, device=dev)
+        sim.launch(n, 0, 1000, sums, ws, status, d_per_run=rec, d_best_height=bh)
+        torch.cuda.synchronize()
+        assert int(status[1]) == 0
+        out.append((sums.cpu(), rec.cpu(), bh.cpu()))
+        del ws
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(out[0], out[2]):
+        assert torch.equal(a, b)
