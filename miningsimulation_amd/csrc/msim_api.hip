@@ -19,7 +19,6 @@
 #include "msim_jump.h"
 #include "msim_kernels.h"
 #include "msim_sel_launch.h"
-#include "msim_selpipe.h"
 #include "msim_wide_launch.h"
 
 namespace {
@@ -67,7 +66,6 @@ struct msim_config {
         int dev;
         uint32_t seg, nseg;
         void *ptr;
-        int kind;  // 0: the honest pipeline's pick table, 1: the selfish pipeline's (msim_selpipe.h)
     };
     std::vector<Tab> tables;  // per (device, segment length) pipeline tables, lazily uploaded
     // Large honest networks (msim_wide.h): any miner count up to WIDE_MAX_M, integer weights summing to W.
@@ -79,8 +77,6 @@ struct msim_config {
     std::vector<std::pair<int, void *>> wtables;  // per device: pick, fast-threshold, prop, log, jump tables
     // Networks with selfish miners (msim_sel.h entity engine): parameter block.
     bool sel = false;
-    bool sp_ok = false;  // the selfish pipeline serves it (msim_selpipe.h: K1<NIB> + S2 instead of E1)
-    double sp_rho = 0;   // its candidate rate
     msim::SelParams sp;
     std::vector<std::pair<int, void *>> stables;  // per device: SelParams + point list {0}
     // Every network, as the general engine reads it: G finishes the runs the entity engine cannot, and
@@ -184,14 +180,9 @@ msim::PipeLayout pipe_layout(const msim_config *c, uint64_t n_runs)
     return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET, draw_slots());
 }
 
-msim::SpLayout sp_layout(const msim_config *c, uint64_t n_runs)
-{
-    return msim::sp_layout_for(c->sp_rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET, draw_slots());
-}
-
 // Pipeline tables for this config on the current device: pick table, log table, jump matrices for
 // draw offsets j * seg.
-int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables *out, int kind = 0)
+int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables *out)
 {
     using namespace msim;
     int dev = 0;
@@ -200,12 +191,11 @@ int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables 
     const size_t pick_b = sizeof(PickTab), log_b = sizeof(LogTab);
     void *d = nullptr;
     for (const auto &t : c->tables)
-        if (t.dev == dev && t.seg == seg && t.nseg >= nseg && t.kind == kind) d = t.ptr;
+        if (t.dev == dev && t.seg == seg && t.nseg >= nseg) d = t.ptr;
     if (!d) {
         const size_t jump_b = (size_t)nseg * 128 * 16;
         std::vector<char> h(pick_b + log_b + jump_b);
-        if (kind == 1) build_pick_table_sp(c->perc, c->prop, c->self, (int)c->n, (PickTab *)h.data());
-        else build_pick_table(c->perc, c->prop, c->self, (int)c->n, (PickTab *)h.data());
+        build_pick_table(c->perc, c->prop, c->self, (int)c->n, (PickTab *)h.data());
         build_log_table((LogTab *)(h.data() + pick_b));
         build_jump_table(nseg, seg, (uint32_t *)(h.data() + pick_b + log_b));
         if (hipMalloc(&d, h.size()) != hipSuccess) return MSIM_E_HIP;
@@ -213,7 +203,7 @@ int device_tables(msim_config *c, uint32_t seg, uint32_t nseg, msim::PipeTables 
             (void)hipFree(d);
             return MSIM_E_HIP;
         }
-        c->tables.push_back({dev, seg, nseg, d, kind});
+        c->tables.push_back({dev, seg, nseg, d});
     }
     const char *b = (const char *)d;
     out->pick = (const PickTab *)b;
@@ -430,21 +420,11 @@ struct SelGroupDev {
     uint32_t uni;  // every point of the group has a uniform propagation delay
 };
 
-// The selfish pipeline of one network (msim_selpipe.h): its layout, device tables and workspace.
-struct SpPlan {
-    msim::SpLayout SL;
-    msim::PipeTables tab;
-    char *ws;
-    uint32_t ps;  // the selfish miner's delay (K1's never-settles mask bit)
-};
-
-// The slice loop of one launch: E1 per group (or, for a network the selfish pipeline serves, K1<NIB> + S2 per
-// slice) -> E2 (retries) -> G (what E2 cannot finish) -> F.
+// The slice loop of one launch: E1 per group -> E2 (retries) -> G (what E2 cannot finish) -> F.
 int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const msim::GenParams *d_gpts,
                     const std::vector<SelGroupDev> &groups, const msim::LogTab *logt, const SelWs &w, char *ws,
                     uint64_t run_begin, uint64_t rpp, uint32_t seed_base, void *d_sums, void *d_per_run,
-                    void *d_best_height, void *d_status, hipStream_t s, std::vector<hipEvent_t> *engine_events,
-                    const SpPlan *sp = nullptr, std::vector<hipEvent_t> *k1_events = nullptr)
+                    void *d_best_height, void *d_status, hipStream_t s, std::vector<hipEvent_t> *engine_events)
 {
     using namespace msim;
     uint32_t *counts = (uint32_t *)(ws + w.counts_off);
@@ -483,78 +463,7 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
     };
     uint32_t max_ns = 1;
     for (const auto &g : groups) max_ns = g.nscls > max_ns ? g.nscls : max_ns;
-    if (sp) {  // K1<NIB> draws every block, S2 applies the settled form per run (msim_selpipe.h)
-        const PipeLayout &L = sp->SL.L;
-        char *pw = sp->ws;
-        DrawArgs da;
-        da.tab = sp->tab;
-        da.seed_base = seed_base;
-        da.nr = L.nr;
-        da.seg = L.seg;
-        da.gps = L.gps;
-        da.nseg = L.nseg;
-        da.cap = L.cap;
-        da.band_lo = L.band_lo;
-        da.lcap = L.lcap;
-        da.lchunk = L.lchunk;
-        da.segsum = (uint64_t *)(pw + L.segsum_off);
-        da.segcnt = (uint32_t *)(pw + L.segcnt_off);
-        da.nslow = (uint32_t *)(pw + L.nslow_off);
-        da.slots = (uint32_t *)(pw + L.slots_off);
-        da.gsum = (uint32_t *)(pw + L.gsum_off);
-        da.gend = (uint64_t *)(pw + L.gend_off);
-        da.gcum = (uint32_t *)(pw + L.gcum_off);
-        da.grec = (GroupRec *)(pw + L.grec_off);
-        da.list = (EpEntry *)(pw + L.list_off);
-        da.list_count = (uint32_t *)(pw + L.count_off);
-        da.nib = (uint32_t *)(pw + sp->SL.nib_off);
-        da.cmask = (CMask *)(pw + sp->SL.cmask_off);
-        da.ps = sp->ps;
-        SpArgs sa;
-        sa.nr = L.nr;
-        sa.seg = L.seg;
-        sa.nsg = L.nsg;
-        sa.nseg = L.nseg;
-        sa.nb = L.nb;
-        sa.cap = L.cap;
-        sa.band_lo = L.band_lo;
-        sa.lcap = L.lcap;
-        sa.segsum = da.segsum;
-        sa.segcnt = da.segcnt;
-        sa.nslow = da.nslow;
-        sa.slots = da.slots;
-        sa.gend = da.gend;
-        sa.gcum = da.gcum;
-        sa.grec = da.grec;
-        sa.list = da.list;
-        sa.nib = da.nib;
-        sa.cmask = da.cmask;
-        sa.stale = (uint32_t *)(pw + sp->SL.stale_off);
-        // engine phases start when 48 of a wave's 64 lanes wait (measured on configs[2]: 16 -> 88.9 ms,
-        // 32 -> 77.8, 48 -> 77.1 per 131 072-run step, profiles/r05/sp); MSIM_SP_XTH overrides (A/B)
-        sa.xth = 48;
-        if (const char *e = getenv("MSIM_SP_XTH")) sa.xth = (uint32_t)atoi(e);
-        a.plist = groups[0].plist;
-        a.nlist = 1;
-        a.uni = groups[0].uni;
-        for (uint64_t s0 = 0; s0 < rpp; s0 += L.nr) {
-            const uint32_t sn = (uint32_t)((rpp - s0) < L.nr ? (rpp - s0) : L.nr);
-            a.s0 = (uint32_t)s0;
-            a.sn = sn;
-            da.run_begin = run_begin + s0;
-            da.n = sn;
-            if (hipMemsetAsync(da.list_count, 0, sizeof(uint32_t), s) != hipSuccess ||
-                hipMemsetAsync(sa.stale, 0, (size_t)L.nb / 32 * L.nr * 4, s) != hipSuccess)
-                return MSIM_E_HIP;
-            event(k1_events);
-            if (launch_draws(da, s) != hipSuccess) return MSIM_E_HIP;
-            event(k1_events);
-            event(engine_events);
-            if (launch_selpipe(a, sa, m, s) != hipSuccess) return MSIM_E_HIP;
-            event(engine_events);
-        }
-    }
-    for (uint64_t s0 = 0; !sp && s0 < rpp; s0 += w.nr) {
+    for (uint64_t s0 = 0; s0 < rpp; s0 += w.nr) {
         const uint32_t sn = (uint32_t)((rpp - s0) < w.nr ? (rpp - s0) : w.nr);
         a.s0 = (uint32_t)s0;
         a.sn = sn;
@@ -827,21 +736,6 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         bool prop_ok = true;
         for (uint32_t k = 0; k < n; ++k) prop_ok = prop_ok && miners[k].propagation_ms < (int64_t)msim::FTHR_CAP;
         c->pipe_ok = !sel && !gen && prop_ok && rho <= PIPE_MAX_RHO && getenv("MSIM_NO_PIPELINE") == nullptr;
-        // The selfish pipeline (msim_selpipe.h): one selfish miner, the settled form (every delay >= 1 ms),
-        // integer percentages (K1's pick table), rare candidates, and a run of at least ~1 000 blocks (its
-        // end search needs a band of groups). Opt-in (MSIM_SELPIPE=1): measured on MI355X it is still slower
-        // than E1 on configs[2] (1.90 M against 2.35 M run-years/s, profiles/r05/INDEX.md), so E1 serves by
-        // default.
-        if (sel && c->sp.macro && c->sp.ns == 1 && total_weight == 100) {
-            c->sp_rho = msim::sp_rho(c->perc, c->prop, c->self, (int)n);
-            bool fits = true;
-            const int64_t ps = miners[c->sp.sids[0]].propagation_ms;
-            for (uint32_t k = 0; k < n; ++k)
-                fits = fits && miners[k].propagation_ms + ps + 1 < (int64_t)msim::FTHR_CAP;
-            c->sp_ok = fits && c->sp_rho <= msim::SP_MAX_RHO && (double)duration_ms / 599999.5 >= 1024.0 &&
-                       getenv("MSIM_SELPIPE") != nullptr && atoi(getenv("MSIM_SELPIPE")) != 0 &&
-                       getenv("MSIM_NO_SELPIPE") == nullptr;
-        }
     } else {
         c->wide = true;
         c->pipe_ok = false;
@@ -927,7 +821,7 @@ size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
     if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->gen_full).total;
     if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
     if (cfg->sel)
-        return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total + (cfg->sp_ok ? sp_layout(cfg, n_runs).total : 0);
+        return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total;
     size_t t = ws_layout(cfg->n, n_runs).total;
     if (cfg->pipe_ok) t += pipe_layout(cfg, n_runs).total;
     return t;
@@ -1015,20 +909,8 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         } else {
             lk.unlock();
         }
-        SpPlan plan;
-        if (cfg->sp_ok) {
-            plan.SL = sp_layout(cfg, n_runs);
-            if (workspace_bytes < w.total + plan.SL.total) return MSIM_E_INVALID;
-            rc = device_tables(c, plan.SL.L.seg, plan.SL.L.nseg, &plan.tab, 1);
-            if (rc) return rc;
-            plan.ws = (char *)d_workspace + w.total;
-            plan.ps = 0;
-            for (uint32_t k = 0; k < cfg->n; ++k)
-                if (cfg->self[k]) plan.ps = (uint32_t)cfg->prop[k];
-        }
         rc = sel_launch_impl(cfg->n, 1, pts, gp, groups, lt, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
-                             d_per_run, d_best_height, d_status, s, on ? &tm.engine : nullptr, cfg->sp_ok ? &plan : nullptr,
-                             on ? &tm.k1 : nullptr);
+                             d_per_run, d_best_height, d_status, s, on ? &tm.engine : nullptr);
         if (le) (void)hipEventRecord(le, s);
         return rc;
     }
@@ -1595,17 +1477,6 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
     }
     if (cfg->sel) {
         const SelWs w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
-        if (cfg->sp_ok) {  // the selfish pipeline: K1<NIB> segments + S2
-            const msim::SpLayout sl = sp_layout(cfg, n_runs);
-            out->uses_pipeline = 5;
-            out->slice_runs = sl.L.nr;
-            out->segment_blocks = sl.L.seg;
-            out->segments = sl.L.nseg;
-            out->blocks_per_run = sl.L.nb;
-            out->workspace_bytes = w.total + sl.total;
-            out->rho = cfg->sp_rho;
-            return MSIM_OK;
-        }
         out->uses_pipeline = 3;
         out->slice_runs = w.nr;  // E1 draws in-lane: no draw segments
         out->segment_blocks = 0;

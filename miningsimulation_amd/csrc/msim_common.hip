@@ -119,19 +119,6 @@ hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream
     }
 }
 
-hipError_t launch_selpipe(const SelArgs &a, const SpArgs &sa, uint32_t m, hipStream_t s)
-{
-    switch (m) {
-#define CASE(MM) \
-    case MM:     \
-        return launch_selpipe_m##MM(a, sa, s);
-        MSIM_FOR_EACH_M(CASE)
-#undef CASE
-    default:
-        return hipErrorInvalidValue;
-    }
-}
-
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s)
 {
     switch (m) {

@@ -13,7 +13,6 @@
 #include "msim_jump.h"
 #include "msim_kernels.h"
 #include "msim_pipeline.h"
-#include "msim_selpipe.h"
 
 namespace msim {
 
@@ -54,16 +53,13 @@ __device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rn
 // aggregated appends to the dense episode list, the band's group records.
 constexpr uint32_t K1_OWNERS = 2 * CNT_WORDS;  // 15 miners + PickFinder's fall-through (index 15)
 constexpr uint32_t K1_NSL = K1_OWNERS;         // LDS row after the owners: the lane's slow-block count
-constexpr uint32_t K1_MA = K1_NSL + 1;         // NIB: the candidate masks of the lane's current group (A, B)
-constexpr uint32_t K1_NW = K1_MA + 2;          // NIB: the group's first three nibble words
-constexpr uint32_t K1_ROWS = K1_NW + 3;
+constexpr uint32_t K1_ROWS = K1_NSL + 1;
 
 // The slow path keeps no per-lane register across the draw loop: its lane-dependent values are rebuilt from
 // the ballot mask (mbcnt), wave-uniform SGPRs and LDS (the per-lane list count), so the loop's register
 // budget (K1_WAVES below) goes to the draws. Measured on MI355X (profiles/r03/INDEX.md): with the lane id,
 // its bit, the list count and the counter address held across the loop, the compiler reloaded them from
 // scratch once per quad (six scratch loads and two vmcnt(0) waits per quad).
-template <bool NIB>
 struct DevCtx {
     const DrawArgs &a;
     uint32_t (*cnt)[256];
@@ -71,7 +67,6 @@ struct DevCtx {
     uint32_t tid, r0, seg, jb;  // r0: the wave's first run (wave-uniform)
     uint32_t cbase;             // tid * 4, rebuilt every quad (quad())
     uint32_t wbase;             // 4 x the wave's first thread (SGPR)
-    uint32_t nibw;              // NIB: the finders of the last 8 blocks, oldest in the low nibble
     __device__ __forceinline__ void quad()
     {
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshl_add_u32 %0, %0, 2, %1"
@@ -84,24 +79,6 @@ struct DevCtx {
         const uint32_t ad = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)&cnt[0][0] +
                             ((info & (15u << INFO_K_SHIFT)) | cbase);
         __atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)ad, 1u, __ATOMIC_RELAXED);
-        if (NIB) nibw = (nibw >> 4) | ((info & (15u << INFO_K_SHIFT)) << (28 - INFO_K_SHIFT));
-    }
-    // NIB: one u32 of 8 finder nibbles per 8 blocks; a group's four words wait in LDS and leave as one 16-byte
-    // store (the chunk layout of msim_selpipe.h) with the group's candidate masks (kept in LDS by slow():
-    // nothing on the fast path)
-    __device__ __forceinline__ void quad_done(uint32_t g, uint32_t q4)
-    {
-        if (!NIB || !(q4 & 1u)) return;
-        if (q4 != GROUP / K1_QB - 1) {
-            cnt[K1_NW + (q4 >> 1)][tid] = nibw;
-            return;
-        }
-        const size_t c = (size_t)seg * (a.seg / GROUP) + g;
-        *(uint4 *)(a.nib + sp_nib_index(a.nr, run(), (uint32_t)c * 4)) =
-            make_uint4(cnt[K1_NW][tid], cnt[K1_NW + 1][tid], cnt[K1_NW + 2][tid], nibw);
-        a.cmask[c * a.nr + run()] = CMask{cnt[K1_MA][tid], cnt[K1_MA + 1][tid]};
-        cnt[K1_MA][tid] = 0;
-        cnt[K1_MA + 1][tid] = 0;
     }
     __device__ __forceinline__ bool vote(bool s) const { return (__builtin_amdgcn_ballot_w64(s) & amask) != 0ull; }
     // the owner counters packed as the u16 pairs of the workspace layout (msim_pipeline.h CNT_WORDS)
@@ -119,8 +96,7 @@ struct DevCtx {
         for (uint32_t i = lane; i < lleft; i += 64u)
             if (lo + i < a.lcap) a.list[lo + i].run = EP_HOLE;
     }
-    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp,
-                         uint32_t fthr)
+    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         const uint64_t mask = __builtin_amdgcn_ballot_w64(s) & amask;
         // rank of this lane among the slow ones (asm volatile: computed here, not hoisted out of the loop)
@@ -161,19 +137,12 @@ struct DevCtx {
         const uint32_t c = *nsl;
         if (c < a.cap) a.slots[((size_t)seg * a.cap + c) * a.nr + r] = idx;
         *nsl = c + 1u;
-        if (NIB) {  // A: listed; B: I_{i+1} <= prop_k (fthr = prop_k + prop_s + 1), a candidate that never settles
-            const uint32_t bit = 1u << (block & (GROUP - 1u));
-            cnt[K1_MA][r & 255u] |= bit;
-            if ((w1 >> 5) + a.ps < fthr) cnt[K1_MA + 1][r & 255u] |= bit;
-        }
     }
     __device__ __forceinline__ uint32_t run() const { return r0 + (tid & 63u); }
-    // NIB: records per super-group (msim_pipeline.h pipe_layout_nr)
     __device__ void group_start(uint32_t g, uint32_t w0, const Rng &ri, const Rng &rp)
     {
-        if (NIB && g % SGROUP) return;
         const uint32_t r = run();
-        const size_t gi = NIB ? (size_t)jb * ((a.gps + SGROUP - 1) / SGROUP) + g / SGROUP : (size_t)jb * a.gps + g;
+        const size_t gi = (size_t)jb * a.gps + g;
         GroupRec gr;
         gr.ri = ri;
         gr.rp = rp;
@@ -185,7 +154,7 @@ struct DevCtx {
     }
     __device__ void group(uint32_t g, uint32_t sum, uint64_t end)
     {
-        if (!NIB) a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum;
+        a.gsum[((size_t)jb * a.gps + g) * a.nr + run()] = sum;
         if (g % SGROUP == SGROUP - 1 || g + 1 == a.gps) {
             const uint32_t nsg = (a.gps + SGROUP - 1) / SGROUP;
             a.gend[((size_t)jb * nsg + g / SGROUP) * a.nr + run()] = end;
@@ -201,9 +170,6 @@ struct DevCtx {
 #ifndef MSIM_K1_WAVES
 #define MSIM_K1_WAVES 5
 #endif
-// NIB: the selfish pipeline's K1 (msim_selpipe.h): every block's finder nibble stored, a block listed when
-// I_{i+1} < fthr (STRICT; its table gives honest finders fthr = prop_k + prop_s + 1, selfish ones 0).
-template <bool NIB>
 #if MSIM_K1_WAVES
 __global__ __launch_bounds__(256, MSIM_K1_WAVES) void msim_draws_kernel(const DrawArgs a)
 #else
@@ -232,10 +198,10 @@ __global__ __launch_bounds__(256) void msim_draws_kernel(const DrawArgs a)
     if (seg) jump2(reinterpret_cast<const uint4 *>(a.tab.jump) + (size_t)seg * 128, ri, rp);
 
     const uint32_t b0 = seg * a.seg;
-    DevCtx<NIB> cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, (uint32_t)__builtin_amdgcn_readfirstlane(r & ~63u), seg,
-                   seg - a.band_lo, 0u,
-                   (uint32_t)__builtin_amdgcn_readfirstlane((tid & ~63u) * 4u), 0u, 0u, 0u};
-    const uint64_t tsum = draw_segment<DevCtx<NIB>, NIB>(cx, ri, rp, &sm.log, &sm.pick, b0, a.seg, seg >= a.band_lo);
+    DevCtx cx{a, s_cnt, __builtin_amdgcn_ballot_w64(r < a.n), tid, (uint32_t)__builtin_amdgcn_readfirstlane(r & ~63u), seg,
+              seg - a.band_lo, 0u,
+              (uint32_t)__builtin_amdgcn_readfirstlane((tid & ~63u) * 4u), 0u, 0u};
+    const uint64_t tsum = draw_segment<DevCtx>(cx, ri, rp, &sm.log, &sm.pick, b0, a.seg, seg >= a.band_lo);
     cx.holes();
     a.segsum[(size_t)seg * a.nr + r] = tsum;
 #pragma unroll
@@ -278,13 +244,12 @@ hipError_t launch_picks(const PickTab *pt, const uint64_t *u, int32_t *out, uint
 
 hipError_t draws_blocks_per_cu(int *blocks)
 {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_draws_kernel<false>, 256, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, msim_draws_kernel, 256, 0);
 }
 
 hipError_t launch_draws(const DrawArgs &a, hipStream_t s)
 {
-    if (a.nib) hipLaunchKernelGGL(msim_draws_kernel<true>, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(msim_draws_kernel<false>, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(msim_draws_kernel, dim3(a.nr / 256, a.nseg), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

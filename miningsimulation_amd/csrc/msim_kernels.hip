@@ -309,9 +309,6 @@ static hipError_t launch_pipeline(const LaunchArgs &a, uint64_t *parts)
     da.band_lo = L.band_lo;
     da.lcap = L.lcap;
     da.lchunk = L.lchunk;
-    da.nib = nullptr;
-    da.cmask = nullptr;
-    da.ps = 0;
     da.segsum = (uint64_t *)(ws + L.segsum_off);
     da.segcnt = (uint32_t *)(ws + L.segcnt_off);
     da.nslow = (uint32_t *)(ws + L.nslow_off);

@@ -63,12 +63,6 @@ struct EpEntry {
     Rng ri, rp;       // both streams, positioned at the block after w1
 };
 
-// The selfish pipeline's candidate masks of one 32-block chunk of a run (msim_selpipe.h): bit i of a = block
-// 32c + i is listed, of b = it is listed and I_{i+1} <= prop_k.
-struct alignas(8) CMask {
-    uint32_t a, b;
-};
-
 // A group of the band (where a run can end): the first block's word and both streams after it.
 struct GroupRec {
     Rng ri, rp;
@@ -117,9 +111,6 @@ struct DrawArgs {
     GroupRec *grec;       // [nband][gps][nr]
     EpEntry *list;        // [lcap]
     uint32_t *list_count;
-    uint32_t *nib;        // selfish pipeline only: finder nibbles, 16-byte chunks of 32 blocks (msim_selpipe.h)
-    CMask *cmask;         // selfish pipeline only: [nb / 32][nr] candidate masks (msim_selpipe.h SpArgs)
-    uint32_t ps;          // selfish pipeline only: the selfish miner's delay
 };
 
 struct PipeArgs {  // K2 / K3
@@ -146,17 +137,15 @@ enum : uint32_t { REC_ENDED = 1u, REC_ERR = 2u, REC_SKIP = 4u };
 // `slots` = wave slots of K1 on the device (CUs x resident waves per CU). The run is cut into `nseg`
 // workers of `seg` blocks so that the K1 grid fills the device in whole rounds: every wave does the
 // same work, so a partial last round would leave SIMDs idle.
-// The layout of a slice of exactly nr runs (a multiple of 256). recs: the honest pipeline (K2's episode
-// records; band records per group). !recs: the selfish pipeline, which reads the list entries themselves and
-// keeps band records (counts and RNG states) per super-group only, and no group sums (msim_selpipe.h sp_begin).
-inline PipeLayout pipe_layout_nr(double rho, uint32_t m, int64_t duration_ms, uint32_t nr, uint32_t slots, bool recs)
+// The layout of a slice of exactly nr runs (a multiple of 256): K2's episode records, band records per group.
+inline PipeLayout pipe_layout_nr(double rho, uint32_t m, int64_t duration_ms, uint32_t nr, uint32_t slots)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     PipeLayout L;
     const double D = (double)duration_ms;
     const double mu = D / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
     const double need = mu + 8.0 * sd + 64.0;  // blocks to pre-generate (P(more) < 1e-15 per run)
-    L.rec_words = recs ? 3 + 2 * m : 0;
+    L.rec_words = 3 + 2 * m;
     L.k2_kind = rho <= K2_LEAN_RHO ? 0u : K2_KIND_HI;
     L.nr = nr;
     // workers per run: minimise rounds(w) * (seg(w) + jump cost), jump ~ 25 blocks of work
@@ -204,9 +193,9 @@ inline PipeLayout pipe_layout_nr(double rho, uint32_t m, int64_t duration_ms, ui
     o = al(o + (size_t)L.nseg * L.nr * 4);
     L.slots_off = o;
     o = al(o + (size_t)L.nseg * L.cap * L.nr * 4);
-    const size_t grp = recs ? L.gps : L.nsg;  // band records per segment
+    const size_t grp = L.gps;  // band records per segment
     L.gsum_off = o;
-    o = al(o + (recs ? (size_t)L.nband * L.gps * L.nr * 4 : 0));
+    o = al(o + (size_t)L.nband * L.gps * L.nr * 4);
     L.gend_off = o;
     o = al(o + (size_t)L.nband * L.nsg * L.nr * 8);
     L.gcum_off = o;
@@ -225,11 +214,11 @@ inline PipeLayout pipe_layout_nr(double rho, uint32_t m, int64_t duration_ms, ui
 
 // The largest slice (all n_runs, or fewer) whose layout, plus extra_per_run bytes per run, fits the budget.
 inline PipeLayout pipe_layout_for(double rho, uint32_t m, int64_t duration_ms, uint64_t n_runs, double budget,
-                                  uint32_t slots, bool recs = true, double extra_per_run = 0.0)
+                                  uint32_t slots, double extra_per_run = 0.0)
 {
     uint64_t nr = (n_runs + 255) / 256 * 256;
     for (;;) {
-        const PipeLayout L = pipe_layout_nr(rho, m, duration_ms, (uint32_t)nr, slots, recs);
+        const PipeLayout L = pipe_layout_nr(rho, m, duration_ms, (uint32_t)nr, slots);
         const double tot = (double)L.total + extra_per_run * (double)nr;
         if (tot <= budget || nr <= 256) return L;
         uint64_t next = (uint64_t)((double)nr * budget / tot * 0.98) / 256 * 256;
@@ -316,23 +305,19 @@ MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, cons
 // One (run, segment) worker: SEG blocks from the jumped RNG states. Ctx supplies the side effects:
 //   count(info)                       per-owner counter of this lane (+1 for owner info_finder(info))
 //   vote(s)                           nonzero when s holds for some active lane of the wave (host: s)
-//   slow(s, block, offset, w0, w1, ri, rp, fthr)
+//   slow(s, block, offset, w0, w1, ri, rp)
 //                                     called after a nonzero vote: records a non-fast block when s
 //                                     (offset = its find time minus the segment's start; its word, the
 //                                     next one and both streams after them; the finder's threshold)
 //   group(g, sum, end)                band only: sum of the group's intervals, and the time from the segment's
 //                                     start to the group's end
 //   quad()                            start of a quad of blocks
-//   quad_done(g, q4)                  after quad q4 of group g (the selfish pipeline's K1 stores its finder
-//                                     nibbles here, msim_selpipe.h; a no-op for honest networks)
 //   group_start(g, w0, ri, rp)        band only: before group g's first block (its word and the streams
 //                                     after it; snapshot the counters)
-// STRICT: a block is listed when I_{i+1} < fthr (the selfish pipeline, whose table gives selfish finders
-// fthr = 0: never listed) instead of I_{i+1} <= fthr (honest networks: fthr = the finder's delay).
 // Blocks are drawn four at a time (draw_quad_fast); the streams after a block inside a quad, needed only
 // by the rare non-fast block, are re-stepped from the quad's start. Time is summed per group in 32 bits
 // (32 intervals < 2^25 ms each) and folded into 64 bits per group.
-template <class Ctx, bool STRICT = false>
+template <class Ctx>
 MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restrict__ lt,
                               const PickTab *__restrict__ pt, uint32_t b0, uint32_t seg, bool band)
 {
@@ -373,7 +358,7 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
 #pragma unroll
             for (int q = 0; q < K1_QB; ++q) {
                 gacc += Icur;
-                const bool slow = STRICT ? I[q] < info_fthr(infocur) : I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
+                const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
                 cx.count(infocur);
                 if (cx.vote(slow)) {
                     Rng a = ri0, b = rp0;  // the streams after block i+1
@@ -382,12 +367,11 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
                         rng_next(b);
                     }
                     cx.slow(slow, b0 + g * GROUP + q4 * K1_QB + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
-                            (I[q] << 5) | info_finder(info[q]), a, b, info_fthr(infocur));
+                            (I[q] << 5) | info_finder(info[q]), a, b);
                 }
                 Icur = I[q];
                 infocur = info[q];
             }
-            cx.quad_done(g, q4);
         }
         if (band) cx.group(g, gacc, tsum + gacc);
         tsum += gacc;

@@ -9,7 +9,6 @@
 #include "msim_reduce.h"
 #include "msim_sel_launch.h"
 #include "msim_selm.h"
-#include "msim_selpipe.h"
 
 namespace msim {
 
@@ -171,9 +170,6 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #endif
 #ifndef SEL_ENGPROF
 #define SEL_ENGPROF 0
-#endif
-#ifndef SP_PROF
-#define SP_PROF 0
 #endif
 #ifndef SEL_MSTEPS
 #define SEL_MSTEPS 2
@@ -441,260 +437,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 #endif
 }
 
-// The selfish pipeline's engine source takes back K1's count of every block below B the engine consumes.
-template <int M>
-struct SpCntDev {
-    uint32_t *c;  // &s_cnt[0][tid]
-    __device__ __forceinline__ void add(uint32_t k, uint32_t v) { atomicAdd(&c[(C_F * M + (int)k) * TPB], v); }
-};
-
-// S2's engine capacities: reveal groups and cold slots (a run that outgrows them is flagged for E2).
-#ifndef SP_NG
-#define SP_NG 4
-#endif
-#ifndef SP_NC
-#define SP_NC SEL_NC
-#endif
-static_assert(SP_NC <= SEL_NC, "S2's cold slots live in the launch's SEL_NC-slot workspace");
-
-// S2 of the selfish pipeline (msim_selpipe.h): one lane per run of the slice, one network (point 0). The
-// lane applies the settled-state transitions from K1's finder nibbles a word at a time through the four-block
-// table (the table phase) until a word needs the block-by-block path (a candidate that needs the engine, B,
-// an error) — then it waits; when sa.xth lanes wait (or no lane is left in the table phase) the wave runs an
-// engine phase: each waiting lane runs its word block by block, enters the engine from K1's stored RNG states
-// if the word asks for it (sp_enter), and is stepped by the entity engine until it hands its run back to the
-// table phase (take_back below B, then the rest of that word block by block) or finishes. The settled state
-// and the cursor wait in LDS during engine phases.
-// Measured on MI355X (profiles/r05/sp): a round-based split into a table-path kernel and a compacted engine
-// kernel, with the run state in global memory between rounds, was 1.9x slower on configs[2] (145 ms against
-// 77 ms per 131 072-run step): with one lane per run the split leaves two waves per SIMD and ~200 rounds of
-// latency-bound launches. Moving the engine phase into a non-inlined function was slower too (97 ms).
-template <int M, bool UNI>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_selpipe_kernel(const SelArgs a,
-                                                                                                            const SpArgs sa)
-{
-    __shared__ uint32_t s_cnt[4 * M][TPB];
-    __shared__ uint32_t s_st[SpCur::NW + SpSt::NW + 1][TPB];  // cursor, settled state, the engine's hand-back block
-    __shared__ uint32_t s_tab[SP_LUT];                         // four-block transitions (msim_selpipe.h sp_lut_entry)
-    __shared__ int64_t s_prop[MAXM];
-    __shared__ uint8_t s_lut[128];
-    __shared__ LogTab s_log[1];
-    const uint32_t tid = threadIdx.x;
-    const SelParams *P = a.pts;
-    if (tid < MAXM) s_prop[tid] = P->prop[tid];
-    if (tid < 128) {
-        uint32_t f = 0;
-        for (int j = 0; j < MAXM; ++j) f += P->ccum[j] <= tid ? 1u : 0u;
-        s_lut[tid] = (uint8_t)f;
-    }
-    if (tid < SP_LUT) s_tab[tid] = sp_lut_entry(tid / 16u, tid % 16u);
-    if (tid < LOG_TAB) {
-        s_log[0].invc[tid] = a.logt->invc[tid];
-        s_log[0].A[tid] = a.logt->A[tid];
-    }
-#pragma unroll
-    for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
-    __syncthreads();
-    const uint32_t lr = blockIdx.x * TPB + tid;  // run of the slice (K1's slice-local index)
-    const bool active = lr < a.sn;
-    const uint32_t rel = a.s0 + lr;
-    SelDevEnv<M, UNI> env{&s_cnt[0][tid], s_prop, P->prop[0], P->uniform_prop != 0, a.cold + (size_t)blockIdx.x * TPB + tid,
-                          a.cold_lanes};
-    const int64_t D = P->duration_ms;
-    const uint32_t sid = P->sids[0];
-    int64_t thr = 0;
-    for (uint32_t k = 0; k < P->m; ++k)
-        if (k != sid) thr = P->prop[k] + P->prop[sid] > thr ? P->prop[k] + P->prop[sid] : thr;
-    const int xth = (int)__builtin_amdgcn_readfirstlane(sa.xth >= 1u && sa.xth <= 64u ? sa.xth : 48u);
-    uint32_t *cs = &s_st[0][tid], *ss = &s_st[SpCur::NW][tid], *hb = &s_st[SpCur::NW + SpSt::NW][tid];
-    // the lane's exact drawer (B's super-group redrawn in the prologue and at an engine entry at B)
-    auto drawer = [&]() {
-        SelFastDraw<M> d;
-        d.lt = s_log;
-        d.lut = s_lut;
-        d.P = P;
-        d.kc = fd_consts();
-        d.wt = false;
-        return d;
-    };
-    SpCur cur;
-    SpSt st;
-    int mode = 3;
-    uint32_t bh = 0, err = 0;
-    if (active) {
-        SelFastDraw<M> drw = drawer();
-        sp_begin(sa, lr, D, thr, drw, cur);
-        st.F = st.h = st.w = st.sst = st.prs = st.pxf = st.smask = st.schunk = st.hbits = 0;
-        err = cur.err | (a.force_retry ? SERR_CAP : 0u);
-        mode = err ? 3 : 0;
-    }
-    auto park = [&](const SelOut &r) {
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-            env.set(C_F, (uint32_t)k, r.found[k]);
-            env.set(C_S, (uint32_t)k, r.stale[k]);
-        }
-        bh = r.best_height;
-        err |= r.err;
-    };
-    auto vote = [](bool b) { return __builtin_amdgcn_ballot_w64(b) != 0ull; };
-    // the block-by-block path of a waiting word; a finished run is parked
-    // (sp_finish writes found / stale into the counters itself; only the height is parked)
-    auto slow = [&]() {
-        mode = sp_slow_word<M>(sa, lr, env, cur, st, sid, D);
-        if (mode == 6) {
-            SelOut r;
-            sp_finish<M>(env, st, sid, r);
-#pragma unroll
-            for (int k = 0; k < M; ++k) {
-                env.set(C_F, (uint32_t)k, r.found[k]);
-                env.set(C_S, (uint32_t)k, r.stale[k]);
-            }
-            bh = st.F + st.h;
-            mode = 3;
-        } else if (mode == 3) {
-            err |= cur.err;
-        }
-    };
-#if SP_PROF  // per-wave phase timing (diagnostic builds only: scripts/build_variant.sh ... -DSP_PROF=1)
-    uint64_t pt_n = 0, pt_e = 0, pn_n = 0, pn_e = 0, pi_n = 0, pi_e = 0, pl_n = 0, pl_e = 0;
-    const uint64_t pt0 = clock64();
-#endif
-    for (;;) {
-        const uint64_t bn = __builtin_amdgcn_ballot_w64(mode == 0);
-        const uint64_t bw = __builtin_amdgcn_ballot_w64((mode == 1) | (mode == 4) | (mode == 9));
-        if ((bn | bw) == 0ull) break;
-#if SP_PROF
-        const uint64_t pc0 = clock64();
-        const bool peng = bw != 0ull && (__builtin_popcountll(bw) >= xth || bn == 0ull);
-#endif
-        if (bw != 0ull && (__builtin_popcountll(bw) >= xth || bn == 0ull)) {
-            if (mode == 9) slow();
-            cur.save(cs, TPB);
-            st.save(ss, TPB);
-            Sel<M, 1, 1, SP_NG, 1, SP_NC> s;
-            SpSrc<SelFifo<SelFastDraw<M>>, SpCntDev<M>> src;
-            src.f.d = drawer();
-            src.f.n = 0;
-            src.cnt.c = &s_cnt[0][tid];
-            src.pidx = SP_NONE;
-            src.pk = 0;
-            src.B = cur.B;
-            if ((mode == 1) | (mode == 4)) {
-                mode = sp_enter<M>(sa, lr, mode, cur, st, src, s, env, P->m, P->sids);
-                if (mode == 3) err |= cur.err;
-                ss[3 * TPB] = st.sst;  // SpSt::sst, flushed by the hand-over
-            }
-            for (;;) {
-                if (mode == 2) {
-                    const bool live = s.step(env, src, D);
-                    if (!live) {
-                        SelOut r;
-                        s.finish(env, D, r);
-                        park(r);
-                        mode = 3;
-                    } else if (src.pidx < src.B) {
-                        SelMacro<M> tb;
-                        if (tb.take_back(env, s, sid)) {  // back to the table phase at src.pidx
-                            SpSt t;
-                            t.load(ss, TPB);
-                            sp_handback<M>(env, tb, t, src.pidx, sid);
-                            t.save(ss, TPB);
-                            hb[0] = src.pidx;
-                            mode = 7;
-                        }
-                    }
-                }
-#if SP_PROF
-                ++pi_e;
-                pl_e += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 2));
-#endif
-                if (__builtin_amdgcn_ballot_w64(mode == 2) == 0ull) break;
-            }
-            cur.load(cs, TPB);
-            st.load(ss, TPB);
-            if (mode == 7) {  // handed back by the engine: the rest of its word block by block
-                sp_seek(sa, lr, cur, hb[0]);
-                mode = 0;
-                if (cur.pos & 7u) slow();
-            }
-            if (mode == 0) sp_refill(sa, lr, cur);  // the chunk ring was not kept through the phase
-        } else {
-            // every lane in mode 0 steps one chunk per table step, from ring slot 0 (the phase follows a refill)
-            bool stop = false;
-            auto step = [&](auto sc) {
-                constexpr int S = decltype(sc)::value % SP_PF;
-                if (stop) return;
-                if (mode == 0) {
-                    mode = sp_chunk<M, S>(sa, lr, env, vote, s_tab, cur, st, sid);
-                    if (mode == 3) err |= cur.err;
-                }
-#if SP_PROF
-                ++pi_n;
-                pl_n += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 0));
-#endif
-                stop = __builtin_amdgcn_ballot_w64(mode == 0) == 0ull ||
-                       __builtin_popcountll(__builtin_amdgcn_ballot_w64((mode == 1) | (mode == 4) | (mode == 9))) >= xth;
-            };
-            while (!stop) {  // four steps per pass: slots 0..3 of the ring (SP_PF divides 4)
-                step(std::integral_constant<int, 0>{});
-                step(std::integral_constant<int, 1>{});
-                step(std::integral_constant<int, 2>{});
-                step(std::integral_constant<int, 3>{});
-            }
-        }
-#if SP_PROF
-        const uint64_t pc1 = clock64();
-        if (peng) {
-            pt_e += pc1 - pc0;
-            ++pn_e;
-        } else {
-            pt_n += pc1 - pc0;
-            ++pn_n;
-        }
-#endif
-    }
-#if SP_PROF
-    if (blockIdx.x < 2 && (threadIdx.x & 63u) == 0u)
-        printf("SPPROF blk %u wave %u total %llu | table phases %llu cyc %llu chunk steps %llu lanes %llu | engine phases %llu cyc %llu iters %llu lanes %llu\n",
-               blockIdx.x, threadIdx.x / 64u, (unsigned long long)(clock64() - pt0), (unsigned long long)pn_n,
-               (unsigned long long)pt_n, (unsigned long long)pi_n, (unsigned long long)pl_n, (unsigned long long)pn_e,
-               (unsigned long long)pt_e, (unsigned long long)pi_e, (unsigned long long)pl_e);
-#endif
-    SelOut o;
-    o.err = err;
-    o.best_height = bh;
-    if (active && !err) {
-        uint32_t F[M], X[M];
-        sp_counts<M>(sa, lr, cur, F);
-        sp_stale_counts<M>(sa, lr, st, sid, X);
-#pragma unroll
-        for (int k = 0; k < M; ++k) {
-            o.found[k] = env.get(C_F, (uint32_t)k) + F[k] - X[k];
-            o.stale[k] = env.get(C_S, (uint32_t)k) + X[k];
-        }
-    }
-    uint64_t v[6 * M];
-#pragma unroll
-    for (int i = 0; i < 6 * M; ++i) v[i] = 0;
-    if (active) {
-        if (o.err) {
-            const uint32_t pos = atomicAdd(a.counts, 1u);
-            if (pos < a.err_cap) a.err_list[pos] = rel;
-        } else {
-            sel_terms<M>(o, v);
-            if (a.records)
-#pragma unroll
-                for (int k = 0; k < M; ++k) {
-                    a.records[2 * ((size_t)rel * M + k) + 0] = o.found[k];
-                    a.records[2 * ((size_t)rel * M + k) + 1] = o.stale[k];
-                }
-            if (a.best_h) a.best_h[rel] = o.best_height;
-        }
-    }
-    block_reduce_store<M>(v, a.partials + ((size_t)a.s0 / TPB + blockIdx.x) * 6 * M);
-}
-
 // E2: one lane per flagged (point, run), wide capacities, draws from the seeds.
 template <int M, int NS>
 __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
@@ -782,13 +524,6 @@ hipError_t MSIM_CAT(launch_sel_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, h
 #else
     return hipErrorInvalidValue;
 #endif
-}
-hipError_t MSIM_CAT(launch_selpipe_m, MSIM_M)(const SelArgs &a, const SpArgs &sa, hipStream_t s)
-{
-    const dim3 grid((a.sn + TPB - 1) / TPB);
-    if (a.uni) hipLaunchKernelGGL((msim_selpipe_kernel<MSIM_M, true>), grid, dim3(TPB), 0, s, a, sa);
-    else hipLaunchKernelGGL((msim_selpipe_kernel<MSIM_M, false>), grid, dim3(TPB), 0, s, a, sa);
-    return hipGetLastError();
 }
 hipError_t MSIM_CAT(launch_sel_retry_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, hipStream_t s)
 {

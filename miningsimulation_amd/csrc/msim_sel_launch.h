@@ -73,12 +73,8 @@ struct SelArgs {
 // E1 / E2 for miner count m and selfish class (1, 2, 4); dispatch in msim_common.hip.
 hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
-struct SpArgs;
-// S2 of the selfish pipeline (msim_selpipe.h) for miner count m: one network, one slice (a.s0, a.sn).
-hipError_t launch_selpipe(const SelArgs &a, const SpArgs &sa, uint32_t m, hipStream_t s);
 #define MSIM_DECL_SEL(MM)                                                                               \
     hipError_t launch_sel_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);                    \
-    hipError_t launch_selpipe_m##MM(const SelArgs &a, const SpArgs &sa, hipStream_t s);                 \
     hipError_t launch_sel_retry_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);
 MSIM_FOR_EACH_M(MSIM_DECL_SEL)
 #undef MSIM_DECL_SEL

@@ -234,7 +234,7 @@ struct SelMacro {
 
     // The settled-state transition of a find by miner k (is_s: k is the selfish miner), applied only when ok
     // (branch-free: every update is masked). It touches no counter: found blocks are counted by the caller
-    // (step: one provisional count per find; the selfish pipeline: by its draw kernel, msim_selpipe.h).
+    // (step: one provisional count per find).
     MSIM_HD void transition(uint32_t k, bool is_s, bool ok, uint32_t sid)
     {
         const bool hon = ok & !is_s;

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r05iter}; mkdir -p $O
 if [ -z "$NOTEST" ]; then
-  timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_selpipe.py tests/test_gpu_selfish.py tests/test_gpu_parity.py} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_selfish.py tests/test_gpu_parity.py} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
   tail -1 $O/pytest.log
 fi
 for c in ${CFGS-c3 c2 c1}; do

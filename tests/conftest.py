@@ -47,13 +47,12 @@ def native_tests():
     wide = os.path.join(ROOT, "build", "libwide_host.so")
     sel = os.path.join(ROOT, "build", "libsel_host.so")
     gen = os.path.join(ROOT, "build", "libgeneral_host.so")
-    sp = os.path.join(ROOT, "build", "libselpipe_host.so")
     kat = os.path.join(ROOT, "build", "libselkat_host.so")
-    outs = (lib, chk, pipe, wide, sel, gen, sp, kat)
+    outs = (lib, chk, pipe, wide, sel, gen, kat)
     if not all(os.path.exists(p) for p in outs) or _stale(outs):
         ge.build_native_tests()
     return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel,
-            "general_host": gen, "selpipe_host": sp, "selkat_host": kat}
+            "general_host": gen, "selkat_host": kat}
 
 
 @pytest.fixture(scope="session")

@@ -31,8 +31,7 @@ struct HostCtx {
     }
     bool vote(bool s) const { return s; }
     void quad() {}
-    void quad_done(uint32_t, uint32_t) {}
-    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp, uint32_t)
+    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
     {
         if (!s) return;
         const uint32_t idx = (uint32_t)list->size();

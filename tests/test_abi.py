@@ -81,21 +81,10 @@ def test_config_validation_without_gpu(msim_lib_path):
                      total_weight=102400)
     assert big.pipeline_info(1024)["uses_pipeline"] == 4
     assert big.workspace_bytes(65536) < 3 * 2**30, big.workspace_bytes(65536)
-    # configs[2] at its per-GPU size: the selfish pipeline (msim_selpipe.h) keeps K1's per-block finder nibbles,
-    # candidate masks, list and band records, and S2's stale masks (~66 KB per run-year, ~8.7 GB of the 288 GB);
-    # E1 alone stays under 1 GiB
-    # (opt-in: MSIM_SELPIPE=1; E1 serves configs[2] by default)
-    import os
+    # configs[2] at its per-GPU size: E1 draws in-lane and keeps its workspace under 1 GiB
     e1 = Simulation(setup_miners(1000, selfish_perc=40))
     assert e1.pipeline_info(131072)["uses_pipeline"] == 3
     assert e1.workspace_bytes(131072) < 2**30
-    os.environ["MSIM_SELPIPE"] = "1"
-    try:
-        c3 = Simulation(setup_miners(1000, selfish_perc=40))
-        assert c3.pipeline_info(131072)["uses_pipeline"] == 5
-        assert c3.workspace_bytes(131072) < 9 * 2**30, c3.workspace_bytes(131072)
-    finally:
-        del os.environ["MSIM_SELPIPE"]
     # the large-network path (msim_wide.h): more than 15 honest miners, or integer weights
     assert Simulation([Miner(k, 7 if k < 10 else 5, 1000) for k in range(16)]).wide
     assert not Simulation(setup_miners()).wide
