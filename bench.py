@@ -35,32 +35,50 @@ BLOCKS_PER_RUN_YEAR = 31_556_952_000 / 600_000  # SIM_DURATION / BLOCK_INTERVAL 
 
 
 # PMC constants of the dominant kernel per launch at the default run counts, from rocprofv3 --pmc passes of
-# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc_r05.sh: FETCH_SIZE, WRITE_SIZE and the SQ
-# set in separate passes; the files hold values summed over the 2 launches, KB). PMC counters cannot be collected
-# inside the timed process: these are the recorded values of the same kernel, and every field computed from them
-# names its file.
+# `bench.py --config C --steps 2 --warmup 0 --streams 1` (scripts/gpu_pmc_r06.sh: FETCH_SIZE, WRITE_SIZE, the SQ
+# issue/stall set, the VALU instruction mix and the VALU busy/lane set in separate passes; scripts/pmc_csv.py writes
+# every counter as its mean per dispatch). PMC counters cannot be collected inside the timed process: these are the
+# recorded values of the same kernel, and every field computed from them names its file.
 #   traffic = FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half the bytes of wide reads, MI355X_MICROARCH.md §HBM)
 #             + WRITE_SIZE, bytes per launch;
 #   valu    = SQ_INSTS_VALU (wave instructions) per launch: the counter-based VALU issue fraction is
-#             valu x 64 lanes / the kernel's time / peak.
-PMC_DIR = "profiles/r05/final/pmc"
+#             valu x 64 lanes / the kernel's time / peak (every instruction priced at one full-rate issue slot);
+#   cycles  = the same instructions priced by class: FP64 FMA/MUL/ADD and f64 conversions at half rate (the MI355X
+#             FP64 vector peak, 78.6 TF, is half the FP32 one), 64-bit integer at half rate, FP64 transcendentals at
+#             1/8, everything else full rate (2 cycles per wave64 instruction on a SIMD-32): frac_cycles is the share
+#             of the SIMDs' cycles those issue costs fill;
+#   lanes   = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64): the active share of a VALU instruction's 64 lanes
+#             (rocprof's VALUUtilization; below 1 = divergence).
+PMC_DIR = "profiles/r06/final/pmc"
 PMC = {
-    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "file": "pmc_c2.txt"},
-    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "file": "pmc_c3.txt"},
-    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "file": "pmc_c5.txt"},
+    ("c1", 32768): {"kernel": "K1 msim_draws_kernel", "file": "pmc_c1.txt", "substr": "msim_draws_kernel"},
+    ("c2", 32768): {"kernel": "K1 msim_draws_kernel", "file": "pmc_c2.txt", "substr": "msim_draws_kernel"},
+    ("c3", 131072): {"kernel": "E1 msim_sel_kernel<9,1,1,4,1,4,true>", "file": "pmc_c3.txt", "substr": "msim_sel_kernel<"},
+    ("c5", 65536): {"kernel": "W1 msim_wide_draws_kernel<4>", "file": "pmc_c5.txt", "substr": "msim_wide_draws_kernel"},
 }
+# issue cycles of one wave64 instruction per class on a SIMD-32 (see `cycles` above)
+CYC_FULL, CYC_HALF, CYC_TRANS64 = 2.0, 4.0, 16.0
+N_SIMD = 256 * 4
+CLOCK_HZ = 2.4e9
 # rocprofv3 --kernel-trace --stats summaries (scripts/rocprof_summary.py) of the exact bench commands: the default
 # two streams (_s0) and --streams 1 (_s1). Their "busy ms/call" column is the union of the kernel's dispatch
 # intervals per call, the file-backed counterpart of the live dominant_ms; the serial file's average is the
 # kernel alone.
-ROCPROF_DIR = "profiles/r05/final"
+ROCPROF_DIR = "profiles/r06/final"
 KERNEL_SUBSTR = {"c1": "msim_draws_kernel", "c2": "msim_draws_kernel", "c3": "msim_sel_kernel<",
                  "c5": "msim_wide_draws_kernel"}
 
 
-def pmc_constants(config: str, n: int) -> dict | None:
-    """{kernel, src, fetch_kb, write_kb, valu} per launch from the committed PMC file (None if absent)."""
-    ent = PMC.get((config, n))
+# Second kernels worth reporting beside the dominant one (same files): c1's episode kernel K2, which takes about
+# as long as K1 at configs[0]'s 1.7 % fork rate.
+PMC_EXTRA = {
+    ("c1", 32768): {"kernel": "K2 msim_episode_kernel<9,1>", "file": "pmc_c1.txt", "substr": "msim_episode_kernel<"},
+}
+
+
+def pmc_constants(config: str, n: int, table: dict | None = None) -> dict | None:
+    """Per-launch PMC values of the config's profiled kernel from the committed file (None if absent)."""
+    ent = (table or PMC).get((config, n))
     if not ent:
         return None
     path = os.path.join(PMC_DIR, ent["file"])
@@ -68,26 +86,44 @@ def pmc_constants(config: str, n: int) -> dict | None:
         txt = open(os.path.join(ROOT, path)).read()
     except OSError:
         return None
-    # scripts/pmc_csv.py format: a header "<kernel>  dispatches=D  mean_ms=..." (D over the three passes), then
-    # "    <COUNTER>  <value summed over the launches of its pass>" lines
-    vals, cur, launches = {}, False, 2
+    # scripts/pmc_csv.py format: "<kernel>  dispatches=D  mean_ms=X  vgpr=..." then "    <COUNTER>  <per dispatch>"
+    vals, cur, head = {}, False, ""
     for ln in txt.splitlines():
+        if ln.startswith("#"):
+            continue
         if not ln.startswith(" "):
-            cur = KERNEL_SUBSTR[config] in ln and not vals
+            cur = ent["substr"] in ln and not vals
             if cur:
-                for tok in ln.split():
-                    if tok.startswith("dispatches=") and int(tok.split("=")[1]) % 3 == 0:
-                        launches = max(1, int(tok.split("=")[1]) // 3)
+                head = ln
             continue
         parts = ln.split()
         if cur and len(parts) == 2:
             vals[parts[0]] = float(parts[1])
-    vals = {k: v / launches for k, v in vals.items()}
     need = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU")
     if not all(k in vals for k in need):
         return None
-    return {"kernel": ent["kernel"], "src": path, "fetch_kb": vals["FETCH_SIZE"], "write_kb": vals["WRITE_SIZE"],
-            "valu": vals["SQ_INSTS_VALU"]}
+    out = {"kernel": ent["kernel"], "src": path, "fetch_kb": vals["FETCH_SIZE"], "write_kb": vals["WRITE_SIZE"],
+           "valu": vals["SQ_INSTS_VALU"], "counters": vals}
+    for tok in head.split():
+        if tok.startswith("mean_ms="):
+            out["profiled_mean_ms"] = float(tok.split("=")[1])
+    mix = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_CVT",
+           "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_TRANS_F64")
+    if all(k in vals for k in mix):
+        half = sum(vals[k] for k in mix[:5])
+        tr = vals["SQ_INSTS_VALU_TRANS_F64"]
+        full = max(vals["SQ_INSTS_VALU"] - half - tr, 0.0)
+        out["issue_cycles"] = (full * CYC_FULL + half * CYC_HALF + tr * CYC_TRANS64) / N_SIMD  # per SIMD per launch
+        out["half_rate_share"] = (half + tr) / vals["SQ_INSTS_VALU"]
+    if vals.get("SQ_ACTIVE_INST_VALU"):
+        if "SQ_THREAD_CYCLES_VALU" in vals:
+            out["valu_utilization"] = vals["SQ_THREAD_CYCLES_VALU"] / (vals["SQ_ACTIVE_INST_VALU"] * 64)
+    if vals.get("GRBM_GUI_ACTIVE") and out.get("profiled_mean_ms"):
+        out["profiled_clock_ghz"] = vals["GRBM_GUI_ACTIVE"] / 8 / (out["profiled_mean_ms"] * 1e-3) / 1e9
+    if vals.get("SQ_WAVE_CYCLES") and vals.get("SQ_WAIT_INST_ANY") is not None:
+        out["wait_inst_share"] = vals["SQ_WAIT_INST_ANY"] / vals["SQ_WAVE_CYCLES"]
+        out["wait_any_share"] = vals.get("SQ_WAIT_ANY", 0.0) / vals["SQ_WAVE_CYCLES"]
+    return out
 
 
 def rocprof_kernel_ms(config: str, streams: int) -> dict | None:
@@ -114,11 +150,17 @@ def w_blk(m: int) -> int:
     return 140 + 4 * math.ceil(math.log2(max(m, 2)))
 
 
-# SURVEY §8(d) calibration of the oracle port against the reference binary: both at 8 threads in the
-# same 8-vCPU build container (Intel Xeon @ 2.1 GHz), c2 at 32 768 runs: the unmodified reference
-# measured 609 run-years/s; the port measured 352.1 run-years/s (oracle_cli time c2
-# 32768 8, 93.08 s). A port figure divided by this ratio estimates the reference binary on the same cores.
+# Calibration of the oracle port against the reference binary (port run-years/s / reference run-years/s on the
+# same cores and config). The reference cannot be built in this image without a stand-in for a library feature
+# libstdc++ 11 lacks (C++20 chrono operator<<), which this project's build rules exclude, so it is
+# never built or timed here; the two measurements on record are:
+#   8 threads: the survey container (8-vCPU Intel Xeon @ 2.1 GHz), c2 at 32 768 runs: reference 609 run-years/s
+#              (BASELINE.md §2), port 352.1 (oracle_cli time c2 32768 8, 93.08 s) -> 0.578;
+#   1 thread:  the round-5 review (Missing #2), c2: reference 65.4 vs port 42.2 -> 0.645.
+# reference_equivalent = port / ratio; the job's threaded sample uses the 8-thread ratio, and the line carries
+# the 1-thread ratio's figure beside it as the spread.
 PORT_TO_REFERENCE = round(352.056 / 609.0, 4)
+PORT_TO_REFERENCE_1T = round(42.2 / 65.4, 4)
 
 
 def cpu_model() -> str:
@@ -190,10 +232,15 @@ def cpu_baseline(preset: str, sample_runs: int, threads: int, visible: int, targ
         "all_cpus_note": f"{threads}-thread rate / {threads} x {visible} visible CPUs: the job may use only its "
                          f"CPU share, so the whole-host figure is extrapolated (linear, an upper bound)",
         "port_to_reference_ratio": PORT_TO_REFERENCE,
+        "port_to_reference_ratio_1thread": PORT_TO_REFERENCE_1T,
         "reference_equivalent": round(rec["run_years_per_s"] / PORT_TO_REFERENCE, 2),
+        "reference_equivalent_spread": [round(rec["run_years_per_s"] / PORT_TO_REFERENCE_1T, 2),
+                                        round(rec["run_years_per_s"] / PORT_TO_REFERENCE, 2)],
         "reference_equivalent_all_visible_cpus": round(per_thread * visible / PORT_TO_REFERENCE, 1),
-        "calibration": "port 352.1 vs reference binary 609 run-years/s, c2, 32768 runs, 8 threads, same container "
-                       "(BASELINE.md §2); reference_equivalent = value / ratio",
+        "calibration": "port/reference on c2: 0.578 at 8 threads (survey container, port 352.1 vs reference 609 "
+                       "run-years/s, BASELINE.md §2) and 0.645 at 1 thread (round-5 review, port 42.2 vs reference "
+                       "65.4); reference_equivalent = value / the 8-thread ratio, spread = value / each ratio. The "
+                       "reference binary is not built here (DESIGN.md §5)",
     }
 
 
@@ -363,9 +410,9 @@ def main() -> None:
         })
     sync()
 
-    def step(i: int):
+    def step(i: int, ln=None):
         begin = (i * world + rank) * n  # disjoint run ranges per step and rank -> fresh seeds
-        ln = lanes[i % ns]
+        ln = ln or lanes[i % ns]
         with on_stream(ln["stream"]):
             sim.launch(n, begin, args.seed_base, ln["sums"], ln["ws"], ln["status"], stream=ln["stream"])
             ln["fails"].add_(ln["status"][1:2].to(torch.int64))
@@ -425,6 +472,33 @@ def main() -> None:
         if not rccl["ok"]:
             raise SystemExit(f"all-reduce check failed: {rccl}")
 
+    # The single-job rate beside the headline: the same steps on ONE stream, each launch waiting for the previous
+    # one (nothing overlaps), timed separately after the headline region with the same barrier + synchronize.
+    serial = None
+    if ns > 1:
+        ks = min(args.steps, 20)
+        for ln in lanes:
+            ln["fails"].zero_()
+        if world > 1:
+            dist.barrier()
+        sync()
+        t1 = time.perf_counter()
+        for i in range(ks):
+            step(args.warmup + args.steps + i, lanes[0])
+        sync()
+        if world > 1:
+            dist.barrier()
+        ts = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        sfails = lanes[0]["fails"].clone()
+        if world > 1:
+            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+            dist.all_reduce(sfails)
+        if int(sfails.item()) != 0:
+            raise SystemExit(f"{int(sfails.item())} runs exceeded the compact state capacity (serial steps)")
+        serial = {"value": round(ks * n * world / float(ts.item()), 1), "steps": ks,
+                  "ms_per_step": round(float(ts.item()) / ks * 1e3, 3),
+                  "how": "the same workload, one HIP stream, one step in flight at a time (timed after the headline)"}
+
     pipe = sim.pipeline_info(n)
     ms_step = elapsed / args.steps * 1e3
     # Roofline of the dominant kernel: the draw kernel for honest networks (K1 / W1: it does every fast block's
@@ -468,14 +542,35 @@ def main() -> None:
             "traffic_source": f"rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of {pmc['kernel']} per launch ({pmc['src']})",
             "valu_per_block": round(pmc["valu"] * 64 / (n * BLOCKS_PER_RUN_YEAR), 2),
         })
+        if "issue_cycles" in pmc:
+            roof.update({
+                "frac_cycles": round(pmc["issue_cycles"] / (dom_ms / 1e3 * CLOCK_HZ), 4),
+                "frac_cycles_how": f"SQ_INSTS_VALU by class ({pmc['src']}): FP64 FMA/MUL/ADD, CVT, INT64 at "
+                                   f"{CYC_HALF:g} cycles, FP64 TRANS at {CYC_TRANS64:g}, the rest at {CYC_FULL:g} "
+                                   f"per wave instruction, / {N_SIMD} SIMDs / (dominant_ms x 2.4 GHz)",
+                "half_rate_share": round(pmc["half_rate_share"], 4),
+            })
+        for key in ("valu_utilization", "profiled_clock_ghz", "wait_inst_share", "wait_any_share"):
+            if key in pmc:
+                roof[key] = round(pmc[key], 4)
         if rp_serial:
             roof.update({
                 "frac_serial": round(pmc["valu"] * 64 / (rp_serial["avg_ms"] / 1e3) / peak, 4),
                 "frac_serial_how": f"same counter over the kernel alone: avg ms in {rp_serial['file']} (--streams 1)",
             })
+            if "issue_cycles" in pmc:
+                roof["frac_cycles_serial"] = round(pmc["issue_cycles"] / (rp_serial["avg_ms"] / 1e3 * CLOCK_HZ), 4)
     else:
         roof.update({"achieved": None, "frac": None, "traffic": None,
-                     "frac_how": "no PMC file for this config / run count (profiles/r05/final/pmc)"})
+                     "frac_how": f"no PMC file for this config / run count / kernel ({PMC_DIR})"})
+    extra = None if args.stub else pmc_constants(args.config, n, PMC_EXTRA)
+    if extra:  # recorded, not timed live: its profiled mean duration and counters
+        roof["second_kernel"] = {
+            "kernel": extra["kernel"], "src": extra["src"], "profiled_mean_ms": extra.get("profiled_mean_ms"),
+            "valu_utilization": round(extra.get("valu_utilization", 0.0), 4),
+            "traffic": round(extra["fetch_kb"] * 1024 * 2 + extra["write_kb"] * 1024),
+            "frac_cycles_profiled": (round(extra["issue_cycles"] / (extra["profiled_mean_ms"] / 1e3 * CLOCK_HZ), 4)
+                                     if "issue_cycles" in extra and extra.get("profiled_mean_ms") else None)}
     # SURVEY 8(d)'s fixed accounting (156 lane-ops per block at M = 9): saturated, because K1 skips the state
     # machine for >99.9 % of blocks; kept for continuity, never the headline.
     roof["frac_convention_per_step"] = round(work / (ms_step / 1e3) / peak, 4)
@@ -519,6 +614,8 @@ def main() -> None:
             },
             "roofline": roof,
         }
+        if serial:
+            line["serial_single_job"] = serial
         if rccl:
             line["rccl"] = rccl
         if args.stub:
