@@ -79,6 +79,10 @@ struct msim_config {
     bool sel = false;
     msim::SelParams sp;
     std::vector<std::pair<int, void *>> stables;  // per device: SelParams + point list {0}
+    // The segment-parallel form of E1 (msim_selseg.h: SW workers + ST stitch) serves it: one selfish miner, the
+    // settled form applies, long runs, rare cuts (seg_rate: expected cuts per find).
+    bool seg_ok = false;
+    double seg_rate = 0;
     // Every network, as the general engine reads it: G finishes the runs the entity engine cannot, and
     // serves alone (`general`) the networks no fast engine covers: selfish miners in networks of more than
     // MSIM_MAX_MINERS miners, more than SEL_MAXS selfish miners, large honest networks whose fork rate the
@@ -354,13 +358,13 @@ struct SelWs {
 constexpr double GEN_FALLBACK_BUDGET = 512.0 * (1 << 20);
 constexpr double GEN_BUDGET = 2048.0 * (1 << 20);
 
-SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
+SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms, uint32_t max_nr = 1u << 22)
 {
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     SelWs w;
     // one slice of every run (up to 2^22 runs per point: cold slots ~1.4 GiB)
     const uint64_t want = (rpp + 255) / 256 * 256;
-    w.nr = (uint32_t)(want < (1ull << 22) ? want : (1ull << 22));
+    w.nr = (uint32_t)(want < max_nr ? want : max_nr);
     w.wpp = (uint32_t)((rpp + msim::TPB - 1) / msim::TPB);
     w.err_cap = (uint32_t)(rpp * np);  // every lane can be retried: the list never overflows
     const size_t nv = 6 * (size_t)m;
@@ -377,6 +381,78 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms)
     w.g = msim::gen_ws_layout(m, duration_ms, w.err_cap, GEN_FALLBACK_BUDGET, true);
     w.total = al(w.gen_off + w.g.total);
     return w;
+}
+
+// Geometry of the segment-parallel form (msim_selseg.h) for slices of nr runs: nseg segments of seg blocks
+// covering mu + 8 sigma + 64 blocks (as K1, msim_pipeline.h), cut into whole rounds of SW's resident waves (92
+// VGPRs: five per SIMD); cap subs per (run, segment) = the expected cuts + 6 sigma + 16 (a run that exceeds it
+// is recomputed by E2); records [nr][nseg][cap] and counts [nseg][nr].
+constexpr double SEG_MAX_RATE = 0.004;             // expected cuts per find above which E1 serves the network
+constexpr double SEG_MIN_BLOCKS = 4096.0;          // shorter runs: E1
+constexpr double SEG_BUDGET = 24.0 * (1ull << 30);  // records of one slice
+struct SegLayout {
+    uint32_t nr, nseg, seg, cap;
+    size_t recs_off, cnt_off, total;
+};
+SegLayout seg_layout_nr(uint32_t m, double rate, int64_t duration_ms, uint32_t nr)
+{
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    SegLayout L;
+    L.nr = nr;
+    const double mu = (double)duration_ms / 599999.5, sd = sqrt(mu > 1.0 ? mu : 1.0);
+    const double need = mu + 8.0 * sd + 64.0;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const double slots = (double)cus * 4.0 * 5.0, rows = ceil(nr / 64.0);
+    uint32_t best = 1;
+    double bestf = 1e300;
+    for (uint32_t w = 1; w <= 64; ++w) {
+        const double sg = ceil(need / w);
+        if (sg < 1024.0 && w > 1) break;
+        const double f = ceil(rows * w / slots) * (sg + 25.0);
+        if (f < bestf * 0.999) {
+            bestf = f;
+            best = w;
+        }
+    }
+    if (const char *e = getenv("MSIM_SEG_NSEG")) best = (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : best;
+    L.nseg = best;
+    L.seg = (uint32_t)ceil(need / best);
+    const double lam = rate * L.seg;
+    L.cap = (uint32_t)ceil(lam + 6.0 * sqrt(lam) + 16.0);
+    L.recs_off = 0;
+    L.cnt_off = al((size_t)nr * L.nseg * L.cap * msim::seg_rec_bytes(m));
+    L.total = al(L.cnt_off + (size_t)L.nseg * nr * 4);
+    return L;
+}
+// Runs per slice of the segment-parallel form: the records of one slice within SEG_BUDGET.
+uint32_t seg_max_nr(uint32_t m, double rate, int64_t duration_ms)
+{
+    const SegLayout L = seg_layout_nr(m, rate, duration_ms, 256);
+    const double per = (double)L.total / 256.0;
+    uint64_t nr = (uint64_t)(SEG_BUDGET / per) / 256 * 256;
+    return (uint32_t)(nr < 256 ? 256 : (nr > (1u << 22) ? (1u << 22) : nr));
+}
+
+// The E1 workspace of a single-network launch, plus the segment-parallel form's records when it serves the config.
+struct SelCfgWs {
+    SelWs w;
+    bool seg;
+    SegLayout L;
+    size_t total;
+};
+SelCfgWs sel_cfg_layout(const msim_config *cfg, uint64_t n_runs)
+{
+    SelCfgWs c;
+    c.seg = cfg->seg_ok;
+    const uint32_t max_nr = c.seg ? seg_max_nr(cfg->n, cfg->seg_rate, cfg->p.duration_ms) : (1u << 22);
+    c.w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, max_nr);
+    c.total = c.w.total;
+    if (c.seg) {
+        c.L = seg_layout_nr(cfg->n, cfg->seg_rate, cfg->p.duration_ms, c.w.nr);
+        c.total += c.L.total;
+    }
+    return c;
 }
 
 // One SelParams for a validated network (weights summing to W, <= MSIM_MAX_MINERS miners).
@@ -420,11 +496,18 @@ struct SelGroupDev {
     uint32_t uni;  // every point of the group has a uniform propagation delay
 };
 
-// The slice loop of one launch: E1 per group -> E2 (retries) -> G (what E2 cannot finish) -> F.
+// The segment-parallel form's device arguments for one launch (msim_selseg.h).
+struct SegPlan {
+    msim::SegArgs g;
+};
+
+// The slice loop of one launch: E1 per group (or SW + ST for a single network the segment-parallel form serves)
+// -> E2 (retries) -> G (what E2 cannot finish) -> F.
 int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const msim::GenParams *d_gpts,
                     const std::vector<SelGroupDev> &groups, const msim::LogTab *logt, const SelWs &w, char *ws,
                     uint64_t run_begin, uint64_t rpp, uint32_t seed_base, void *d_sums, void *d_per_run,
-                    void *d_best_height, void *d_status, hipStream_t s, std::vector<hipEvent_t> *engine_events)
+                    void *d_best_height, void *d_status, hipStream_t s, std::vector<hipEvent_t> *engine_events,
+                    const SegPlan *seg = nullptr)
 {
     using namespace msim;
     uint32_t *counts = (uint32_t *)(ws + w.counts_off);
@@ -468,8 +551,15 @@ int sel_launch_impl(uint32_t m, uint32_t np, const msim::SelParams *d_pts, const
         a.s0 = (uint32_t)s0;
         a.sn = sn;
         event(engine_events);
+        if (seg) {  // one network: SW over (run, segment), then ST per run
+            a.plist = groups[0].plist;
+            a.nlist = 1;
+            a.uni = groups[0].uni;
+            if (launch_segwork(a, seg->g, m, s) != hipSuccess || launch_stitch(a, seg->g, m, s) != hipSuccess)
+                return MSIM_E_HIP;
+        }
         for (const auto &g : groups) {
-            if (!g.nlist) continue;
+            if (!g.nlist || seg) continue;
             a.plist = g.plist;
             a.nlist = g.nlist;
             a.uni = g.uni;
@@ -716,6 +806,18 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
         if (sel) {
             c->sel = true;
             build_sel_params(miners, n, duration_ms, total_weight, &c->sp);
+            if (c->sp.macro && c->sp.ns == 1) {  // expected cuts per find (msim_selseg.h): honest finds that may
+                const uint32_t sid = c->sp.sids[0];  // need the engine (next find within prop_k + prop_s)
+                double rate = 0.0;
+                for (uint32_t k = 0; k < n; ++k)
+                    if (k != sid)
+                        rate += (double)miners[k].perc / (double)total_weight *
+                                (1.0 - exp(-((double)miners[k].propagation_ms + (double)miners[sid].propagation_ms + 1.0) /
+                                           599999.5));
+                c->seg_rate = rate;
+                c->seg_ok = rate <= SEG_MAX_RATE && (double)duration_ms / 599999.5 >= SEG_MIN_BLOCKS &&
+                            getenv("MSIM_NO_SELSEG") == nullptr;
+            }
             c->p.duration_ms = duration_ms;
             c->p.m = (int32_t)n;
             c->p.selfish = (int32_t)c->sp.sids[0];
@@ -821,7 +923,7 @@ size_t msim_workspace_bytes(const msim_config *cfg, uint64_t n_runs)
     if (cfg->general) return gen_only_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, cfg->gen_full).total;
     if (cfg->wide) return 256 + wide_layout(cfg, n_runs).total;
     if (cfg->sel)
-        return sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms).total;
+        return sel_cfg_layout(cfg, n_runs).total;
     size_t t = ws_layout(cfg->n, n_runs).total;
     if (cfg->pipe_ok) t += pipe_layout(cfg, n_runs).total;
     return t;
@@ -880,9 +982,25 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
         return rc;
     }
     if (cfg->sel) {
-        const SelWs w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
-        if (workspace_bytes < w.total) return MSIM_E_INVALID;
+        const SelCfgWs cw = sel_cfg_layout(cfg, n_runs);
+        const SelWs &w = cw.w;
+        if (workspace_bytes < cw.total) return MSIM_E_INVALID;
         msim_config *c = const_cast<msim_config *>(cfg);
+        SegPlan plan;
+        if (cw.seg) {  // the segment-parallel form: jump matrices for offsets j * seg, records after E1's workspace
+            msim::PipeTables tab;
+            const int rt = device_tables(c, cw.L.seg, cw.L.nseg, &tab);
+            if (rt) return rt;
+            plan.g.jump = tab.jump;
+            plan.g.recs = (char *)d_workspace + w.total + cw.L.recs_off;
+            plan.g.cnt = (uint32_t *)((char *)d_workspace + w.total + cw.L.cnt_off);
+            plan.g.nr = cw.L.nr;
+            plan.g.nseg = cw.L.nseg;
+            plan.g.seg = cw.L.seg;
+            plan.g.cap = cw.L.cap;
+            plan.g.xth = 16;
+            if (const char *e = getenv("MSIM_SEG_XTH")) plan.g.xth = (uint32_t)atoi(e);
+        }
         const msim::SelParams *pts = nullptr;
         const uint32_t *plist = nullptr;
         int rc = sel_config_tables(c, &pts, &plist);
@@ -910,7 +1028,7 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
             lk.unlock();
         }
         rc = sel_launch_impl(cfg->n, 1, pts, gp, groups, lt, w, (char *)d_workspace, run_begin, n_runs, seed_base, d_sums,
-                             d_per_run, d_best_height, d_status, s, on ? &tm.engine : nullptr);
+                             d_per_run, d_best_height, d_status, s, on ? &tm.engine : nullptr, cw.seg ? &plan : nullptr);
         if (le) (void)hipEventRecord(le, s);
         return rc;
     }
@@ -1476,13 +1594,21 @@ int msim_pipeline_info(const msim_config *cfg, uint64_t n_runs, msim_pipeline_la
         return MSIM_OK;
     }
     if (cfg->sel) {
-        const SelWs w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms);
-        out->uses_pipeline = 3;
-        out->slice_runs = w.nr;  // E1 draws in-lane: no draw segments
+        const SelCfgWs cw = sel_cfg_layout(cfg, n_runs);
+        out->slice_runs = cw.w.nr;
+        out->workspace_bytes = cw.total;
+        if (cw.seg) {  // the segment-parallel form (msim_selseg.h): SW segments + ST
+            out->uses_pipeline = 6;
+            out->segment_blocks = cw.L.seg;
+            out->segments = cw.L.nseg;
+            out->blocks_per_run = cw.L.nseg * cw.L.seg;
+            out->rho = cfg->seg_rate;
+            return MSIM_OK;
+        }
+        out->uses_pipeline = 3;  // E1 draws in-lane: no draw segments
         out->segment_blocks = 0;
         out->segments = 0;
         out->blocks_per_run = 0;
-        out->workspace_bytes = w.total;
         return MSIM_OK;
     }
     if (!cfg->pipe_ok) return MSIM_OK;

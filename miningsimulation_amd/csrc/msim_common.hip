@@ -3,6 +3,7 @@
 
 #include "msim_kernels.h"
 #include "msim_sel_launch.h"
+#include "msim_selseg.h"
 
 namespace msim {
 
@@ -116,6 +117,45 @@ hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream
 #undef CASE
     default:
         return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_segwork(const SelArgs &a, const SegArgs &g, uint32_t m, hipStream_t s)
+{
+    switch (m) {
+#define CASE(MM) \
+    case MM:     \
+        return launch_segwork_m##MM(a, g, s);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_stitch(const SelArgs &a, const SegArgs &g, uint32_t m, hipStream_t s)
+{
+    switch (m) {
+#define CASE(MM) \
+    case MM:     \
+        return launch_stitch_m##MM(a, g, s);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+size_t seg_rec_bytes(uint32_t m)
+{
+    switch (m) {
+#define CASE(MM) \
+    case MM:     \
+        return sizeof(SegRec<MM>);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return 0;
     }
 }
 

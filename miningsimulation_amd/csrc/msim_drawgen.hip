@@ -19,35 +19,6 @@ namespace msim {
 __device__ __noinline__ int32_t interval_ms_exact_dev(uint64_t u) { return (int32_t)interval_ms_of(u); }
 
 
-// Both RNG states of the lane advanced by the same jump matrix (128 wave-uniform columns).
-__device__ __forceinline__ void jump2(const uint4 *__restrict__ cols, Rng &a, Rng &b)
-{
-    const uint32_t sa[4] = {(uint32_t)a.s0, (uint32_t)(a.s0 >> 32), (uint32_t)a.s1, (uint32_t)(a.s1 >> 32)};
-    const uint32_t sb[4] = {(uint32_t)b.s0, (uint32_t)(b.s0 >> 32), (uint32_t)b.s1, (uint32_t)(b.s1 >> 32)};
-    uint32_t oa0 = 0, oa1 = 0, oa2 = 0, oa3 = 0, ob0 = 0, ob1 = 0, ob2 = 0, ob3 = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-#pragma unroll 8
-        for (int i = 0; i < 32; ++i) {
-            const uint4 c = cols[w * 32 + i];
-            const uint32_t ma = 0u - ((sa[w] >> i) & 1u), mb = 0u - ((sb[w] >> i) & 1u);
-            // o ^= c & m as one v_bitop3_b32 (table of (src0 & src1) ^ src2: 0xF0 & 0xCC ^ 0xAA = 0x6A)
-            oa0 = __builtin_amdgcn_bitop3_b32(c.x, ma, oa0, 0x6A);
-            oa1 = __builtin_amdgcn_bitop3_b32(c.y, ma, oa1, 0x6A);
-            oa2 = __builtin_amdgcn_bitop3_b32(c.z, ma, oa2, 0x6A);
-            oa3 = __builtin_amdgcn_bitop3_b32(c.w, ma, oa3, 0x6A);
-            ob0 = __builtin_amdgcn_bitop3_b32(c.x, mb, ob0, 0x6A);
-            ob1 = __builtin_amdgcn_bitop3_b32(c.y, mb, ob1, 0x6A);
-            ob2 = __builtin_amdgcn_bitop3_b32(c.z, mb, ob2, 0x6A);
-            ob3 = __builtin_amdgcn_bitop3_b32(c.w, mb, ob3, 0x6A);
-        }
-    }
-    a.s0 = (uint64_t)oa0 | ((uint64_t)oa1 << 32);
-    a.s1 = (uint64_t)oa2 | ((uint64_t)oa3 << 32);
-    b.s0 = (uint64_t)ob0 | ((uint64_t)ob1 << 32);
-    b.s1 = (uint64_t)ob2 | ((uint64_t)ob3 << 32);
-}
-
 // Side effects of one K1 lane (msim_pipeline.h draw_segment): LDS per-owner counters (one u32 per owner
 // and lane, [owner][lane]: conflict-free, and the increment is one ds_add_u32 of a constant), wave-
 // aggregated appends to the dense episode list, the band's group records.

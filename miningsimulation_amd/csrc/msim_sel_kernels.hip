@@ -5,10 +5,12 @@
 #include <type_traits>
 
 #include "msim_general_launch.h"
+#include "msim_jump.h"
 #include "msim_kernels.h"
 #include "msim_reduce.h"
 #include "msim_sel_launch.h"
 #include "msim_selm.h"
+#include "msim_selseg.h"
 
 namespace msim {
 
@@ -437,6 +439,255 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 #endif
 }
 
+
+// ------------------------------------------------------------------ segment-parallel form (msim_selseg.h)
+// The per-network tables every selfish kernel keeps in LDS (E1's prologue): delays, PickFinder code table,
+// interval log table, four-find transition table.
+template <int M>
+struct SelLds {
+    uint32_t tab[SP_LUT];
+    int64_t prop[MAXM];
+    uint8_t lut[128];
+    LogTab log;
+    __device__ void load(const SelParams *P, const LogTab *lt, uint32_t tid)
+    {
+        if (tid < SP_LUT) tab[tid] = sp_lut_entry(tid / 16u, tid % 16u);
+        if (tid < MAXM) prop[tid] = P->prop[tid];
+        if (tid < 128) {
+            uint32_t f = 0;
+            for (int j = 0; j < MAXM; ++j) f += P->ccum[j] <= tid ? 1u : 0u;
+            lut[tid] = (uint8_t)f;
+        }
+        if (tid < LOG_TAB) {
+            log.invc[tid] = lt->invc[tid];
+            log.A[tid] = lt->A[tid];
+        }
+    }
+};
+
+template <int M>
+__device__ __forceinline__ void sel_thresholds(const SelParams *P, uint32_t &sid, int64_t &ps, int64_t &thrmax)
+{
+    sid = P->sids[0];
+    ps = P->prop[sid];
+    thrmax = 0;
+    for (uint32_t j = 0; j < P->m; ++j)
+        if (j != sid) thrmax = P->prop[j] + ps > thrmax ? P->prop[j] + ps : thrmax;
+}
+
+// SW: one lane per (run of the slice, segment): the settled form from the quiet state at the segment's first
+// block, with no end of run; a sub per cut and one at the segment's end (msim_selseg.h seg_work). Grid
+// (sn / TPB, nseg): a wave is 64 consecutive runs at one segment, so the jump matrix columns are wave-uniform.
+template <int M, bool UNI>
+__global__ __launch_bounds__(TPB) void msim_segwork_kernel(const SelArgs a, const SegArgs g)
+{
+    __shared__ uint32_t s_cnt[2 * M][TPB];
+    __shared__ SelLds<M> sl;
+    const uint32_t tid = threadIdx.x;
+    const SelParams *P = a.pts + a.plist[0];
+    sl.load(P, a.logt, tid);
+#pragma unroll
+    for (int i = 0; i < 2 * M; ++i) s_cnt[i][tid] = 0u;
+    __syncthreads();
+    const uint32_t lr = blockIdx.x * TPB + tid;  // run of the slice
+    const uint32_t j = blockIdx.y;               // segment
+    if (lr >= a.sn) return;
+    const uint64_t run = a.run_begin + a.s0 + lr;
+    SegFifo<SelFastDraw<M>> src;
+    src.d.ri = rng_seed(seed_interval(a.seed_base, run));
+    src.d.rp = rng_seed(seed_picker(a.seed_base, run));
+    if (j) jump2(reinterpret_cast<const uint4 *>(g.jump) + (size_t)j * 128, src.d.ri, src.d.rp);
+    src.d.lt = &sl.log;
+    src.d.lut = sl.lut;
+    src.d.P = P;
+    src.d.kc = fd_consts();
+    src.d.wt = P->W != 100u;
+    src.n = 0;
+    src.idx = j * g.seg;
+    SelDevEnv<M, UNI> env{&s_cnt[0][tid], sl.prop, P->prop[0], P->uniform_prop != 0, nullptr, 0};
+    uint32_t sid;
+    int64_t ps, thrmax;
+    sel_thresholds<M>(P, sid, ps, thrmax);
+    SegRec<M> *out = (SegRec<M> *)g.recs + ((size_t)lr * g.nseg + j) * g.cap;
+    uint32_t q = 0;
+    auto emit = [&](const SegRec<M> &r) {
+        if (q >= g.cap) return false;
+        out[q++] = r;
+        return true;
+    };
+    const uint32_t err = seg_work<M>(env, src, (j + 1) * g.seg, sid, ps, thrmax, sl.tab, emit);
+    g.cnt[(size_t)j * g.nr + lr] = err ? SEG_OVERFLOW : q;
+}
+
+// The workers' subs of one run, for ST (msim_selseg.h seg_stitch_step's Recs).
+template <int M>
+struct SegDevRecs {
+    const SegRec<M> *recs;  // this run's [nseg][cap]
+    const uint32_t *cnt;    // [nseg][nr], offset to this run
+    uint32_t nseg, cap, nr;
+    __device__ uint32_t count(uint32_t j) const { return j < nseg ? cnt[(size_t)j * nr] : 0u; }
+    __device__ SegRec<M> rec(uint32_t j, uint32_t q) const { return recs[(size_t)j * cap + q]; }
+};
+
+// ST: one lane per run of the slice. Lanes walk their subs (msim_selseg.h seg_stitch_step: jumps, the worker's
+// replay beside the true state, the end of the run); a lane whose true state needs the entity engine waits, and
+// when g.xth lanes of the wave wait (or nothing else is left) the wave runs an engine phase for them, as E1 does.
+// Outputs are E1's: MinerStats terms per workgroup, per-run records, flagged runs for E2.
+template <int M, bool UNI>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_stitch_kernel(const SelArgs a,
+                                                                                                           const SegArgs g)
+{
+    __shared__ uint32_t s_cnt[6 * M][TPB];  // the true C_F, C_S, C_A, C_B; the replayed worker's C_F, C_S
+    __shared__ SelLds<M> sl;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t point = a.plist[0];
+    const SelParams *P = a.pts + point;
+    sl.load(P, a.logt, tid);
+#pragma unroll
+    for (int i = 0; i < 6 * M; ++i) s_cnt[i][tid] = 0u;
+    __syncthreads();
+    const uint32_t lr = blockIdx.x * TPB + tid;
+    const bool active = lr < a.sn;
+    const uint32_t rel = a.s0 + lr;
+    const uint64_t run = a.run_begin + rel;
+    const int64_t D = P->duration_ms;
+    uint32_t sid;
+    int64_t ps, thrmax;
+    sel_thresholds<M>(P, sid, ps, thrmax);
+    SelDevEnv<M, UNI> env{&s_cnt[0][tid], sl.prop, P->prop[0], P->uniform_prop != 0, a.cold + (size_t)blockIdx.x * TPB + tid,
+                          a.cold_lanes};
+    SelDevEnv<M, UNI> envw{&s_cnt[4 * M][tid], sl.prop, P->prop[0], P->uniform_prop != 0, nullptr, 0};
+    SegDevRecs<M> R{(const SegRec<M> *)g.recs + (size_t)(active ? lr : 0) * g.nseg * g.cap, g.cnt + (active ? lr : 0),
+                    g.nseg, g.cap, g.nr};
+    auto make_src = [&]() {
+        SegFifo<SelFastDraw<M>> s;
+        s.d.ri = rng_seed(seed_interval(a.seed_base, run));
+        s.d.rp = rng_seed(seed_picker(a.seed_base, run));
+        s.d.lt = &sl.log;
+        s.d.lut = sl.lut;
+        s.d.P = P;
+        s.d.kc = fd_consts();
+        s.d.wt = P->W != 100u;
+        s.n = 0;
+        s.idx = 0;
+        return s;
+    };
+    SegFifo<SelFastDraw<M>> st = make_src(), sw = make_src();
+    SegStitch<M> S;
+    S.err = 0;
+    S.seg = S.q = 0;
+    S.wnew = 0;
+    S.walk_back = 1;
+    S.WT0 = 0;
+    S.mode = ST_DONE;
+    uint32_t bh = 0, fin = 0;  // fin: the result is parked in the C_F / C_S rows
+    auto park = [&](const SelOut &r) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            env.set(C_F, (uint32_t)k, r.found[k]);
+            env.set(C_S, (uint32_t)k, r.stale[k]);
+        }
+        bh = r.best_height;
+        S.err |= r.err;
+        fin = 1;
+    };
+    if (active) {
+        bool over = a.force_retry != 0;
+        for (uint32_t j = 0; j < g.nseg; ++j) over |= R.count(j) == SEG_OVERFLOW;
+        if (over) {
+            S.err = SERR_CAP;
+        } else if (!S.X.begin(st)) {
+            S.err = SERR_DRAWS;
+        } else if (S.X.T >= D) {
+            SelOut r;
+            S.X.finish(env, sid, r);
+            park(r);
+        } else {
+            seg_set_quiet<M>(S.W, S.X.k, 0);
+            S.mode = ST_JUMP;
+        }
+    }
+    const int xth = (int)__builtin_amdgcn_readfirstlane(g.xth >= 1u && g.xth <= 64u ? g.xth : 16u);
+    for (;;) {
+        const uint64_t bm = __builtin_amdgcn_ballot_w64(S.mode <= ST_WALK || S.mode == ST_END);
+        const uint64_t be = __builtin_amdgcn_ballot_w64(S.mode == ST_ENGINE);
+        if ((bm | be) == 0ull) break;
+        if (be != 0ull && (__builtin_popcountll(be) >= xth || bm == 0ull)) {
+            Sel<M, 1, 1, 4, 1, SEL_NC> s;
+            uint32_t in = S.mode == ST_ENGINE ? 1u : 0u;
+            if (in) S.X.to_exact(env, s, P->m, P->sids);
+            for (;;) {
+                if (in) {
+                    const bool live = s.step(env, st, D);
+                    if (!live) {
+                        SelOut r;
+                        s.finish(env, D, r);
+                        park(r);
+                        S.mode = ST_DONE;
+                        in = 0;
+                    } else if (S.X.take_back(env, s, sid)) {
+                        in = 0;
+                        if (S.X.T >= D) {
+                            SelOut r;
+                            S.X.finish(env, sid, r);
+                            park(r);
+                            S.mode = ST_DONE;
+                        } else {
+                            st.fill();
+                            seg_after_engine<M>(S, R, envw, sw);
+                        }
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(in != 0u) == 0ull) break;
+            }
+        } else {
+            for (;;) {
+                if (S.mode <= ST_WALK || S.mode == ST_END) {
+                    seg_stitch_step<M>(S, R, env, envw, st, sw, D, sid, ps, thrmax, sl.tab);
+                    if (S.mode == ST_DONE && !S.err) {
+                        SelOut r;
+                        S.X.finish(env, sid, r);
+                        park(r);
+                    }
+                }
+                if (__builtin_amdgcn_ballot_w64(S.mode <= ST_WALK || S.mode == ST_END) == 0ull ||
+                    __builtin_popcountll(__builtin_amdgcn_ballot_w64(S.mode == ST_ENGINE)) >= xth)
+                    break;
+            }
+        }
+    }
+    SelOut o;
+    o.err = S.err;
+    o.best_height = bh;
+    if (active && !S.err) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            o.found[k] = env.get(C_F, (uint32_t)k);
+            o.stale[k] = env.get(C_S, (uint32_t)k);
+        }
+    }
+    uint64_t v[6 * M];
+#pragma unroll
+    for (int i = 0; i < 6 * M; ++i) v[i] = 0;
+    if (active) {
+        if (o.err || !fin) {
+            const uint32_t pos = atomicAdd(a.counts, 1u);
+            if (pos < a.err_cap) a.err_list[pos] = point * a.rpp + rel;
+        } else {
+            sel_terms<M>(o, v);
+            const size_t gi = (size_t)point * a.rpp + rel;
+            if (a.records)
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    a.records[2 * (gi * M + k) + 0] = o.found[k];
+                    a.records[2 * (gi * M + k) + 1] = o.stale[k];
+                }
+            if (a.best_h) a.best_h[gi] = o.best_height;
+        }
+    }
+    block_reduce_store<M>(v, a.partials + ((size_t)point * a.wpp + a.s0 / TPB + blockIdx.x) * 6 * M);
+}
+
 // E2: one lane per flagged (point, run), wide capacities, draws from the seeds.
 template <int M, int NS>
 __global__ __launch_bounds__(TPB) void msim_sel_retry_kernel(const SelArgs a)
@@ -524,6 +775,20 @@ hipError_t MSIM_CAT(launch_sel_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, h
 #else
     return hipErrorInvalidValue;
 #endif
+}
+hipError_t MSIM_CAT(launch_segwork_m, MSIM_M)(const SelArgs &a, const SegArgs &g, hipStream_t s)
+{
+    const dim3 grid((a.sn + TPB - 1) / TPB, g.nseg);
+    if (a.uni) hipLaunchKernelGGL((msim_segwork_kernel<MSIM_M, true>), grid, dim3(TPB), 0, s, a, g);
+    else hipLaunchKernelGGL((msim_segwork_kernel<MSIM_M, false>), grid, dim3(TPB), 0, s, a, g);
+    return hipGetLastError();
+}
+hipError_t MSIM_CAT(launch_stitch_m, MSIM_M)(const SelArgs &a, const SegArgs &g, hipStream_t s)
+{
+    const dim3 grid((a.sn + TPB - 1) / TPB);
+    if (a.uni) hipLaunchKernelGGL((msim_stitch_kernel<MSIM_M, true>), grid, dim3(TPB), 0, s, a, g);
+    else hipLaunchKernelGGL((msim_stitch_kernel<MSIM_M, false>), grid, dim3(TPB), 0, s, a, g);
+    return hipGetLastError();
 }
 hipError_t MSIM_CAT(launch_sel_retry_m, MSIM_M)(const SelArgs &a, uint32_t ns_class, hipStream_t s)
 {

@@ -70,12 +70,29 @@ struct SelArgs {
     uint32_t uni;           // every point of this E1 launch has one propagation delay for all miners
 };
 
-// E1 / E2 for miner count m and selfish class (1, 2, 4); dispatch in msim_common.hip.
+// Segment-parallel form of E1 for one network with one selfish miner (msim_selseg.h): SW workers over (run,
+// segment), then ST stitches each run; ST writes E1's outputs (partials, records, flagged runs for E2).
+struct SegArgs {
+    const uint32_t *jump;  // nseg jump matrices, 128 uint4 columns each (msim_jump.h build_jump_table, offsets j*seg)
+    void *recs;            // [nr][nseg][cap] SegRec<M> (msim_selseg.h)
+    uint32_t *cnt;         // [nseg][nr] subs per (segment, run); SEG_OVERFLOW: the worker ran out of room
+    uint32_t nr, nseg, seg, cap;
+    uint32_t xth;          // ST: waiting lanes that start an engine phase
+};
+constexpr uint32_t SEG_OVERFLOW = 0xFFFFFFFFu;
+
+// E1 / E2 for miner count m and selfish class (1, 2, 4); SW / ST for miner count m; dispatch in msim_common.hip.
 hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
+hipError_t launch_segwork(const SelArgs &a, const SegArgs &g, uint32_t m, hipStream_t s);
+hipError_t launch_stitch(const SelArgs &a, const SegArgs &g, uint32_t m, hipStream_t s);
+// bytes of one SegRec<m>
+size_t seg_rec_bytes(uint32_t m);
 #define MSIM_DECL_SEL(MM)                                                                               \
     hipError_t launch_sel_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);                    \
-    hipError_t launch_sel_retry_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);
+    hipError_t launch_sel_retry_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);             \
+    hipError_t launch_segwork_m##MM(const SelArgs &a, const SegArgs &g, hipStream_t s);                 \
+    hipError_t launch_stitch_m##MM(const SelArgs &a, const SegArgs &g, hipStream_t s);
 MSIM_FOR_EACH_M(MSIM_DECL_SEL)
 #undef MSIM_DECL_SEL
 // F: out[p][i] = sum over the point's workgroup partials + its retried runs; status from counts.

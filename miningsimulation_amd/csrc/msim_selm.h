@@ -145,6 +145,8 @@ struct SelFifo {
     }
     MSIM_HD void prefetch() {}
     MSIM_HD void settle() {}
+    // step4 consumed the four held draws (three finds and the new pending one)
+    MSIM_HD void took4() { n = 0u; }
 };
 
 template <int M>
@@ -329,7 +331,7 @@ struct SelMacro {
         }
         T = T3 + (int64_t)In[3];
         k = src.k3;
-        src.n = 0u;
+        src.took4();
         src.fill();
         return T < D ? 0 : 2;
     }

@@ -48,11 +48,12 @@ def native_tests():
     sel = os.path.join(ROOT, "build", "libsel_host.so")
     gen = os.path.join(ROOT, "build", "libgeneral_host.so")
     kat = os.path.join(ROOT, "build", "libselkat_host.so")
-    outs = (lib, chk, pipe, wide, sel, gen, kat)
+    seg = os.path.join(ROOT, "build", "libselseg_host.so")
+    outs = (lib, chk, pipe, wide, sel, gen, kat, seg)
     if not all(os.path.exists(p) for p in outs) or _stale(outs):
         ge.build_native_tests()
     return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel,
-            "general_host": gen, "selkat_host": kat}
+            "general_host": gen, "selkat_host": kat, "selseg_host": seg}
 
 
 @pytest.fixture(scope="session")
