@@ -204,10 +204,10 @@ typedef struct msim_pipeline_layout {
     uint32_t uses_pipeline;   /* 1: event-skipping pipeline (honest network); 2: large-network pipeline;
                                  3: entity engine (selfish miners); 4: general engine (slice_runs = its
                                  lanes, segment_blocks = its first window, segments = window tiers,
-                                 blocks_per_run = its last window); 6: segment-parallel selfish runs (one
-                                 selfish miner: settled-form workers per segment + per-run stitch, rho = the
-                                 expected cuts per find); 0: per-lane kernel (5 was the removed selfish
-                                 pipeline) */
+                                 blocks_per_run = its last window); 6: segment-parallel selfish runs
+                                 (opt-in, environment MSIM_SELSEG=1; one selfish miner: settled-form workers
+                                 per segment + per-run stitch, rho = the expected cuts per find); 0: per-lane
+                                 kernel (5 was the removed selfish pipeline) */
     uint32_t slice_runs;      /* runs per pipeline slice */
     uint32_t segment_blocks;  /* blocks per draw-kernel worker */
     uint32_t segments;        /* workers per run */

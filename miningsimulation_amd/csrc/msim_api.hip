@@ -79,8 +79,9 @@ struct msim_config {
     bool sel = false;
     msim::SelParams sp;
     std::vector<std::pair<int, void *>> stables;  // per device: SelParams + point list {0}
-    // The segment-parallel form of E1 (msim_selseg.h: SW workers + ST stitch) serves it: one selfish miner, the
-    // settled form applies, long runs, rare cuts (seg_rate: expected cuts per find).
+    // The segment-parallel form of E1 (msim_selseg.h: SW workers + ST stitch) serves it when asked for
+    // (MSIM_SELSEG): one selfish miner, the settled form applies, long runs, rare cuts (seg_rate: expected cuts
+    // per find).
     bool seg_ok = false;
     double seg_rate = 0;
     // Every network, as the general engine reads it: G finishes the runs the entity engine cannot, and
@@ -384,15 +385,17 @@ SelWs sel_ws_layout(uint32_t m, uint32_t np, uint64_t rpp, int64_t duration_ms, 
 }
 
 // Geometry of the segment-parallel form (msim_selseg.h) for slices of nr runs: nseg segments of seg blocks
-// covering mu + 8 sigma + 64 blocks (as K1, msim_pipeline.h), cut into whole rounds of SW's resident waves (92
-// VGPRs: five per SIMD); cap subs per (run, segment) = the expected cuts + 6 sigma + 16 (a run that exceeds it
-// is recomputed by E2); records [nr][nseg][cap] and counts [nseg][nr].
+// covering mu + 8 sigma + 64 blocks (as K1, msim_pipeline.h), cut into whole rounds of SW's resident waves (five
+// per SIMD); cap subs per (run, segment) = the expected cuts + 6 sigma + 16 (a run that exceeds it is
+// recomputed by E2), qcap checkpoints (msim_sel_launch.h seg_qcap; measured on configs[2]: ~1 700 per year-long
+// run, ~2/3 of the room; beyond it a worker just stores no more). Records [nr][nseg][cap], checkpoints
+// [nr][nseg][qcap], counts [nseg][nr].
 constexpr double SEG_MAX_RATE = 0.004;             // expected cuts per find above which E1 serves the network
 constexpr double SEG_MIN_BLOCKS = 4096.0;          // shorter runs: E1
 constexpr double SEG_BUDGET = 24.0 * (1ull << 30);  // records of one slice
 struct SegLayout {
-    uint32_t nr, nseg, seg, cap;
-    size_t recs_off, cnt_off, total;
+    uint32_t nr, nseg, seg, cap, qcap;
+    size_t recs_off, cnt_off, qrecs_off, qcnt_off, total;
 };
 SegLayout seg_layout_nr(uint32_t m, double rate, int64_t duration_ms, uint32_t nr)
 {
@@ -420,18 +423,25 @@ SegLayout seg_layout_nr(uint32_t m, double rate, int64_t duration_ms, uint32_t n
     L.seg = (uint32_t)ceil(need / best);
     const double lam = rate * L.seg;
     L.cap = (uint32_t)ceil(lam + 6.0 * sqrt(lam) + 16.0);
+    L.qcap = msim::seg_qcap((uint32_t)ceil(lam), L.seg);
     L.recs_off = 0;
     L.cnt_off = al((size_t)nr * L.nseg * L.cap * msim::seg_rec_bytes(m));
-    L.total = al(L.cnt_off + (size_t)L.nseg * nr * 4);
+    L.qrecs_off = al(L.cnt_off + (size_t)L.nseg * nr * 4);
+    L.qcnt_off = al(L.qrecs_off + (size_t)nr * L.nseg * L.qcap * msim::seg_qrec_bytes(m));
+    L.total = al(L.qcnt_off + (size_t)L.nseg * nr * 4);
     return L;
 }
 // Runs per slice of the segment-parallel form: the records of one slice within SEG_BUDGET.
-uint32_t seg_max_nr(uint32_t m, double rate, int64_t duration_ms)
+uint32_t seg_max_nr(uint32_t m, double rate, int64_t duration_ms, uint64_t n_runs)
 {
-    const SegLayout L = seg_layout_nr(m, rate, duration_ms, 256);
-    const double per = (double)L.total / 256.0;
-    uint64_t nr = (uint64_t)(SEG_BUDGET / per) / 256 * 256;
-    return (uint32_t)(nr < 256 ? 256 : (nr > (1u << 22) ? (1u << 22) : nr));
+    uint64_t nr = (n_runs + 255) / 256 * 256;
+    if (nr > (1u << 22)) nr = 1u << 22;
+    for (;;) {  // the geometry depends on the slice size: shrink until one slice's records fit the budget
+        const SegLayout L = seg_layout_nr(m, rate, duration_ms, (uint32_t)nr);
+        if ((double)L.total <= SEG_BUDGET || nr <= 256) return (uint32_t)nr;
+        uint64_t next = (uint64_t)((double)nr * SEG_BUDGET / (double)L.total * 0.98) / 256 * 256;
+        nr = next >= nr ? nr - 256 : (next < 256 ? 256 : next);
+    }
 }
 
 // The E1 workspace of a single-network launch, plus the segment-parallel form's records when it serves the config.
@@ -445,7 +455,7 @@ SelCfgWs sel_cfg_layout(const msim_config *cfg, uint64_t n_runs)
 {
     SelCfgWs c;
     c.seg = cfg->seg_ok;
-    const uint32_t max_nr = c.seg ? seg_max_nr(cfg->n, cfg->seg_rate, cfg->p.duration_ms) : (1u << 22);
+    const uint32_t max_nr = c.seg ? seg_max_nr(cfg->n, cfg->seg_rate, cfg->p.duration_ms, n_runs) : (1u << 22);
     c.w = sel_ws_layout(cfg->n, 1, n_runs, cfg->p.duration_ms, max_nr);
     c.total = c.w.total;
     if (c.seg) {
@@ -815,8 +825,9 @@ int config_create_impl(const msim_miner *miners, uint32_t n, int64_t duration_ms
                                 (1.0 - exp(-((double)miners[k].propagation_ms + (double)miners[sid].propagation_ms + 1.0) /
                                            599999.5));
                 c->seg_rate = rate;
+                // opt-in (MSIM_SELSEG=1): exact, but slower than E1 on configs[2]
                 c->seg_ok = rate <= SEG_MAX_RATE && (double)duration_ms / 599999.5 >= SEG_MIN_BLOCKS &&
-                            getenv("MSIM_NO_SELSEG") == nullptr;
+                            getenv("MSIM_SELSEG") != nullptr;
             }
             c->p.duration_ms = duration_ms;
             c->p.m = (int32_t)n;
@@ -994,10 +1005,13 @@ int msim_launch(const msim_config *cfg, uint64_t run_begin, uint64_t n_runs, uin
             plan.g.jump = tab.jump;
             plan.g.recs = (char *)d_workspace + w.total + cw.L.recs_off;
             plan.g.cnt = (uint32_t *)((char *)d_workspace + w.total + cw.L.cnt_off);
+            plan.g.qrecs = (char *)d_workspace + w.total + cw.L.qrecs_off;
+            plan.g.qcnt = (uint32_t *)((char *)d_workspace + w.total + cw.L.qcnt_off);
             plan.g.nr = cw.L.nr;
             plan.g.nseg = cw.L.nseg;
             plan.g.seg = cw.L.seg;
             plan.g.cap = cw.L.cap;
+            plan.g.qcap = cw.L.qcap;
             plan.g.xth = 16;
             if (const char *e = getenv("MSIM_SEG_XTH")) plan.g.xth = (uint32_t)atoi(e);
         }

@@ -158,6 +158,19 @@ size_t seg_rec_bytes(uint32_t m)
         return 0;
     }
 }
+uint32_t seg_qcap(uint32_t cuts, uint32_t seg) { return (cuts + 1u) * (SEG_QWIN * 3u / 4u) + seg / SEG_QEVERY + 16u; }
+size_t seg_qrec_bytes(uint32_t m)
+{
+    switch (m) {
+#define CASE(MM) \
+    case MM:     \
+        return sizeof(SegQRec<MM>);
+        MSIM_FOR_EACH_M(CASE)
+#undef CASE
+    default:
+        return 0;
+    }
+}
 
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s)
 {

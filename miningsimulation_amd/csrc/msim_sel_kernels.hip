@@ -509,42 +509,69 @@ __global__ __launch_bounds__(TPB) void msim_segwork_kernel(const SelArgs a, cons
     int64_t ps, thrmax;
     sel_thresholds<M>(P, sid, ps, thrmax);
     SegRec<M> *out = (SegRec<M> *)g.recs + ((size_t)lr * g.nseg + j) * g.cap;
+    SegQRec<M> *qout = (SegQRec<M> *)g.qrecs + ((size_t)lr * g.nseg + j) * g.qcap;
     uint32_t q = 0;
     auto emit = [&](const SegRec<M> &r) {
         if (q >= g.cap) return false;
         out[q++] = r;
         return true;
     };
-    const uint32_t err = seg_work<M>(env, src, (j + 1) * g.seg, sid, ps, thrmax, sl.tab, emit);
+    struct EmitQ {
+        SegQRec<M> *p;
+        uint32_t cap, c;
+        __device__ bool operator()(const SegQRec<M> &r)
+        {
+            if (c >= cap) return false;
+            p[c++] = r;
+            return true;
+        }
+        __device__ uint32_t n() const { return c; }
+    } emitq{qout, g.qcap, 0u};
+    const uint32_t err = seg_work<M>(env, src, (j + 1) * g.seg, sid, ps, thrmax, sl.tab, emit, emitq);
     g.cnt[(size_t)j * g.nr + lr] = err ? SEG_OVERFLOW : q;
+    g.qcnt[(size_t)j * g.nr + lr] = emitq.c;
 }
 
-// The workers' subs of one run, for ST (msim_selseg.h seg_stitch_step's Recs).
+// The workers' subs and checkpoints of one run, for ST (msim_selseg.h seg_stitch_step's Recs).
 template <int M>
 struct SegDevRecs {
-    const SegRec<M> *recs;  // this run's [nseg][cap]
-    const uint32_t *cnt;    // [nseg][nr], offset to this run
-    uint32_t nseg, cap, nr;
+    const SegRec<M> *recs;    // this run's [nseg][cap]
+    const uint32_t *cnt;      // [nseg][nr], offset to this run
+    const SegQRec<M> *qrecs;  // this run's [nseg][qcap]
+    const uint32_t *qcnt;     // [nseg][nr], offset to this run
+    uint32_t nseg, cap, qcap, nr;
     __device__ uint32_t count(uint32_t j) const { return j < nseg ? cnt[(size_t)j * nr] : 0u; }
     __device__ SegRec<M> rec(uint32_t j, uint32_t q) const { return recs[(size_t)j * cap + q]; }
+    __device__ void head(uint32_t j, uint32_t q, uint32_t &b, uint32_t &flags) const
+    {
+        const uint2 v = *(const uint2 *)&recs[(size_t)j * cap + q].b;
+        b = v.x;
+        flags = v.y;
+    }
+    __device__ uint32_t qcount(uint32_t j) const { return j < nseg ? qcnt[(size_t)j * nr] : 0u; }
+    __device__ uint32_t qc(uint32_t j, uint32_t i) const { return qrecs[(size_t)j * qcap + i].c; }
+    __device__ uint32_t qspan(uint32_t j, uint32_t i) const { return qrecs[(size_t)j * qcap + i].span; }
+    __device__ SegQRec<M> qrec(uint32_t j, uint32_t i) const { return qrecs[(size_t)j * qcap + i]; }
 };
 
-// ST: one lane per run of the slice. Lanes walk their subs (msim_selseg.h seg_stitch_step: jumps, the worker's
-// replay beside the true state, the end of the run); a lane whose true state needs the entity engine waits, and
-// when g.xth lanes of the wave wait (or nothing else is left) the wave runs an engine phase for them, as E1 does.
-// Outputs are E1's: MinerStats terms per workgroup, per-run records, flagged runs for E2.
+// ST: one lane per run of the slice. Lanes walk their runs through the workers' records (msim_selseg.h
+// seg_stitch_step: walks to a join, jumps, the end of the run); a lane whose true state needs the entity engine
+// waits, and when g.xth lanes of the wave wait (or nothing else is left) the wave runs an engine phase for them,
+// as E1 does, with every lane's settled state parked in LDS. Outputs are E1's: MinerStats terms per workgroup,
+// per-run records, flagged runs for E2.
 template <int M, bool UNI>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 8))) void msim_stitch_kernel(const SelArgs a,
                                                                                                            const SegArgs g)
 {
-    __shared__ uint32_t s_cnt[6 * M][TPB];  // the true C_F, C_S, C_A, C_B; the replayed worker's C_F, C_S
+    __shared__ uint32_t s_cnt[4 * M][TPB];             // C_F, C_S, C_A, C_B
+    __shared__ uint32_t s_x[SelMacro<M>::NW][TPB];     // the settled state during engine phases
     __shared__ SelLds<M> sl;
     const uint32_t tid = threadIdx.x;
     const uint32_t point = a.plist[0];
     const SelParams *P = a.pts + point;
     sl.load(P, a.logt, tid);
 #pragma unroll
-    for (int i = 0; i < 6 * M; ++i) s_cnt[i][tid] = 0u;
+    for (int i = 0; i < 4 * M; ++i) s_cnt[i][tid] = 0u;
     __syncthreads();
     const uint32_t lr = blockIdx.x * TPB + tid;
     const bool active = lr < a.sn;
@@ -556,29 +583,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
     sel_thresholds<M>(P, sid, ps, thrmax);
     SelDevEnv<M, UNI> env{&s_cnt[0][tid], sl.prop, P->prop[0], P->uniform_prop != 0, a.cold + (size_t)blockIdx.x * TPB + tid,
                           a.cold_lanes};
-    SelDevEnv<M, UNI> envw{&s_cnt[4 * M][tid], sl.prop, P->prop[0], P->uniform_prop != 0, nullptr, 0};
-    SegDevRecs<M> R{(const SegRec<M> *)g.recs + (size_t)(active ? lr : 0) * g.nseg * g.cap, g.cnt + (active ? lr : 0),
-                    g.nseg, g.cap, g.nr};
-    auto make_src = [&]() {
-        SegFifo<SelFastDraw<M>> s;
-        s.d.ri = rng_seed(seed_interval(a.seed_base, run));
-        s.d.rp = rng_seed(seed_picker(a.seed_base, run));
-        s.d.lt = &sl.log;
-        s.d.lut = sl.lut;
-        s.d.P = P;
-        s.d.kc = fd_consts();
-        s.d.wt = P->W != 100u;
-        s.n = 0;
-        s.idx = 0;
-        return s;
-    };
-    SegFifo<SelFastDraw<M>> st = make_src(), sw = make_src();
+    const uint32_t rr = active ? lr : 0u;
+    SegDevRecs<M> R{(const SegRec<M> *)g.recs + (size_t)rr * g.nseg * g.cap, g.cnt + rr,
+                    (const SegQRec<M> *)g.qrecs + (size_t)rr * g.nseg * g.qcap, g.qcnt + rr, g.nseg, g.cap, g.qcap, g.nr};
+    SegFifo<SelFastDraw<M>> st;
+    st.d.ri = rng_seed(seed_interval(a.seed_base, run));
+    st.d.rp = rng_seed(seed_picker(a.seed_base, run));
+    st.d.lt = &sl.log;
+    st.d.lut = sl.lut;
+    st.d.P = P;
+    st.d.kc = fd_consts();
+    st.d.wt = P->W != 100u;
+    st.n = 0;
+    st.idx = 0;
     SegStitch<M> S;
     S.err = 0;
-    S.seg = S.q = 0;
-    S.wnew = 0;
+    S.seg = S.q = S.qi = S.at_rec = 0;
     S.walk_back = 1;
-    S.WT0 = 0;
     S.mode = ST_DONE;
     uint32_t bh = 0, fin = 0;  // fin: the result is parked in the C_F / C_S rows
     auto park = [&](const SelOut &r) {
@@ -603,8 +624,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
             S.X.finish(env, sid, r);
             park(r);
         } else {
-            seg_set_quiet<M>(S.W, S.X.k, 0);
-            S.mode = ST_JUMP;
+            S.mode = ST_WALK;  // segment 0's worker starts quiet at the run's first find
         }
     }
     const int xth = (int)__builtin_amdgcn_readfirstlane(g.xth >= 1u && g.xth <= 64u ? g.xth : 16u);
@@ -613,9 +633,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         const uint64_t be = __builtin_amdgcn_ballot_w64(S.mode == ST_ENGINE);
         if ((bm | be) == 0ull) break;
         if (be != 0ull && (__builtin_popcountll(be) >= xth || bm == 0ull)) {
+            // the settled states wait in LDS while the engine runs; an engine lane converts its state first and
+            // parks the one it hands back
             Sel<M, 1, 1, 4, 1, SEL_NC> s;
-            uint32_t in = S.mode == ST_ENGINE ? 1u : 0u;
+            uint32_t in = S.mode == ST_ENGINE ? 1u : 0u, after = 0u;
             if (in) S.X.to_exact(env, s, P->m, P->sids);
+            else S.X.save(&s_x[0][tid], TPB);
             for (;;) {
                 if (in) {
                     const bool live = s.step(env, st, D);
@@ -625,25 +648,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
                         park(r);
                         S.mode = ST_DONE;
                         in = 0;
-                    } else if (S.X.take_back(env, s, sid)) {
-                        in = 0;
-                        if (S.X.T >= D) {
-                            SelOut r;
-                            S.X.finish(env, sid, r);
-                            park(r);
-                            S.mode = ST_DONE;
-                        } else {
-                            st.fill();
-                            seg_after_engine<M>(S, R, envw, sw);
+                    } else {
+                        SelMacro<M> tb;
+                        if (tb.take_back(env, s, sid)) {
+                            in = 0;
+                            if (tb.T >= D) {
+                                SelOut r;
+                                tb.finish(env, sid, r);
+                                park(r);
+                                S.mode = ST_DONE;
+                            } else {
+                                tb.save(&s_x[0][tid], TPB);
+                                after = 1u;
+                            }
                         }
                     }
                 }
                 if (__builtin_amdgcn_ballot_w64(in != 0u) == 0ull) break;
             }
+            S.X.load(&s_x[0][tid], TPB);
+            if (after) {
+                st.fill();
+                S.mode = S.walk_back ? ST_WALK : ST_END;
+            }
         } else {
             for (;;) {
                 if (S.mode <= ST_WALK || S.mode == ST_END) {
-                    seg_stitch_step<M>(S, R, env, envw, st, sw, D, sid, ps, thrmax, sl.tab);
+                    seg_stitch_step<M>(S, R, env, st, D, sid, ps, thrmax, sl.tab);
                     if (S.mode == ST_DONE && !S.err) {
                         SelOut r;
                         S.X.finish(env, sid, r);

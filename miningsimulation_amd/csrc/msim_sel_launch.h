@@ -76,7 +76,9 @@ struct SegArgs {
     const uint32_t *jump;  // nseg jump matrices, 128 uint4 columns each (msim_jump.h build_jump_table, offsets j*seg)
     void *recs;            // [nr][nseg][cap] SegRec<M> (msim_selseg.h)
     uint32_t *cnt;         // [nseg][nr] subs per (segment, run); SEG_OVERFLOW: the worker ran out of room
-    uint32_t nr, nseg, seg, cap;
+    void *qrecs;           // [nr][nseg][qcap] SegQRec<M>: the workers' quiet checkpoints
+    uint32_t *qcnt;        // [nseg][nr] checkpoints per (segment, run)
+    uint32_t nr, nseg, seg, cap, qcap;
     uint32_t xth;          // ST: waiting lanes that start an engine phase
 };
 constexpr uint32_t SEG_OVERFLOW = 0xFFFFFFFFu;
@@ -86,8 +88,12 @@ hipError_t launch_sel(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream
 hipError_t launch_sel_retry(const SelArgs &a, uint32_t m, uint32_t ns_class, hipStream_t s);
 hipError_t launch_segwork(const SelArgs &a, const SegArgs &g, uint32_t m, hipStream_t s);
 hipError_t launch_stitch(const SelArgs &a, const SegArgs &g, uint32_t m, hipStream_t s);
-// bytes of one SegRec<m>
+// bytes of one SegRec<m> / SegQRec<m>
 size_t seg_rec_bytes(uint32_t m);
+size_t seg_qrec_bytes(uint32_t m);
+// checkpoint room per (run, segment) for the expected cuts of seg blocks (msim_selseg.h SEG_QWIN, SEG_QEVERY):
+// 3/4 of a quiet window per sub + one per SEG_QEVERY blocks + 16; a worker that fills it stores no more
+uint32_t seg_qcap(uint32_t cuts, uint32_t seg);
 #define MSIM_DECL_SEL(MM)                                                                               \
     hipError_t launch_sel_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);                    \
     hipError_t launch_sel_retry_m##MM(const SelArgs &a, uint32_t ns_class, hipStream_t s);             \

@@ -77,13 +77,14 @@ struct SegRec {
     uint32_t flags;    // SEG_CUT / SEG_END
     uint32_t h, w;     // settled state at b
     uint32_t kb;       // finder of block b
-    uint32_t dFh;      // increase of the common prefix F over the sub
+    uint32_t dFh;      // increase of the common prefix F since the sub's last checkpoint (or its start)
+    uint32_t qn;       // the segment's checkpoints before the next sub
     uint32_t n;        // held draws
     uint32_t I[4], k[4];
-    uint64_t span;     // time from the sub's first pending find to find b
+    uint64_t span;     // time from the sub's last checkpoint (or its first pending find) to find b
     uint64_t pend[NP];
     Rng ri, rp;        // the streams after the held draws
-    uint32_t dF[M], dS[M];  // counter deltas over the sub (C_F, C_S), stale blocks flushed at b
+    uint32_t dF[M], dS[M];  // counter deltas since then (C_F, C_S), stale blocks flushed at b
 };
 
 template <int M>
@@ -134,37 +135,95 @@ MSIM_HD void seg_resume(Src &src, const SegRec<M> &r)
     src.fill();
 }
 
+// A worker's quiet checkpoint: its pending find c is quiet (h = w = 0, no honest branch). The true state joins
+// the worker at a block where both are quiet. The worker records every quiet block within the first SEG_QWIN
+// finds after a (re)start (where the true state usually joins: after an engine episode or at a segment start),
+// and after that the first quiet block past every multiple of SEG_QEVERY, so that a late join is never much
+// more than SEG_QEVERY blocks away (measured on configs[2] with the window alone: 7 % of the joins walked to the
+// next cut, ~600 blocks). A checkpoint holds the counter / F / time deltas since the previous checkpoint of its
+// sub (the sub's end record too), so the stitch that joins at a checkpoint adds the later ones and the record's.
+// Checkpoints are an optimisation: when the deltas do not fit or the caller has no room, the sub's later
+// checkpoints are dropped (its record's deltas then reach back to the last one stored) and ST walks further.
+constexpr uint32_t SEG_QWIN = 24, SEG_QEVERY = 64;
+template <int M>
+struct SegQRec {
+    uint32_t c;
+    uint32_t span;          // time since the previous checkpoint of the sub (its start for the first)
+    uint8_t dFh;            // F since then
+    uint8_t dF[M], dS[M];   // counter deltas since then (stale blocks flushed)
+};
+
 // SW lane body: the worker of one segment, blocks [first, e) (src positioned at draw `first`, src.idx = first).
-// Env: the worker's counter rows C_F / C_S (zero at entry), prop_tab. emit(rec) stores a sub; returns false when
-// the caller cannot hold it (the run is then recomputed by E2). Returns 0 or an SERR_* code.
-template <int M, class Env, class Src, class Emit>
+// Env: the worker's counter rows C_F / C_S (zero at entry), prop_tab. emit(rec) / emitq(qrec) store a sub's end
+// record / a quiet checkpoint and return false when the caller cannot hold it (a record: the run is then
+// recomputed by E2; a checkpoint: the sub stores no more);
+// nq() is the number of checkpoints stored so far (SegRec::qn). Inside a quiet window, and from a multiple of
+// SEG_QEVERY to the next quiet block, the worker steps one find at a time (it must see every pending block);
+// elsewhere four. Returns 0 or an SERR_* code.
+template <int M, class Env, class Src, class Emit, class EmitQ>
 MSIM_HD uint32_t seg_work(Env &env, Src &src, uint32_t e, uint32_t sid, int64_t ps, int64_t thrmax, const uint32_t *lut,
-                          Emit &emit)
+                          Emit &emit, EmitQ &emitq)
 {
     SelMacro<M> mc;
     if (!mc.begin(src)) return SERR_DRAWS;
-    int64_t T0 = mc.T;
-    SegRec<M> r;
+    int64_t Tq = mc.T;  // the time of the last checkpoint (or of the sub's start)
+    uint32_t Fq = 0;
+    uint32_t qleft = SEG_QWIN, qnext = 0xFFFFFFFFu;
+    bool qon = true;
     for (;;) {
         const uint32_t i = src.idx - 1u;
         uint32_t fl = 0;
         if (i >= e) {
             fl = SEG_END;
         } else {
-            const int x = (i + 4u <= e) ? mc.step4(env, src, SEG_NO_END, sid, ps, thrmax, lut)
-                                        : mc.step1(env, src, SEG_NO_END, sid, ps);
+            if (qleft == 0u && qnext == 0xFFFFFFFFu) qnext = (i / SEG_QEVERY + 1u) * SEG_QEVERY;  // window over
+            if (qleft != 0u || i >= qnext) {
+                qleft -= qleft != 0u ? 1u : 0u;
+                if (qon && seg_quiet<M>(mc)) {
+                    if (i >= qnext) qnext = (i / SEG_QEVERY + 1u) * SEG_QEVERY;
+                    mc.flush_stale(env, sid);
+                    SegQRec<M> qr;
+                    qr.c = i;
+                    const int64_t dt = mc.T - Tq;
+                    qr.span = (uint32_t)dt;
+                    qr.dFh = (uint8_t)(mc.F - Fq);
+                    bool fits = dt >= 0 && dt <= 0xFFFFFFFFll && mc.F - Fq <= 255u;
+#pragma unroll
+                    for (int kk = 0; kk < M; ++kk) {  // the rows hold the deltas: they restart at every checkpoint
+                        const uint32_t f = env.get(C_F, (uint32_t)kk), x = env.get(C_S, (uint32_t)kk);
+                        fits &= (f <= 255u) & (x <= 255u);
+                        qr.dF[kk] = (uint8_t)f;
+                        qr.dS[kk] = (uint8_t)x;
+                    }
+                    if (fits && emitq(qr)) {
+                        Tq = mc.T;
+                        Fq = mc.F;
+#pragma unroll
+                        for (int kk = 0; kk < M; ++kk) {
+                            env.set(C_F, (uint32_t)kk, 0u);
+                            env.set(C_S, (uint32_t)kk, 0u);
+                        }
+                    } else {
+                        qon = false;  // no more checkpoints in this sub: the record's deltas reach back to the last
+                    }
+                }
+            }
+            const bool one = (qon & (qleft != 0u || i >= qnext)) || i + 4u > e;
+            const int x = one ? mc.step1(env, src, SEG_NO_END, sid, ps) : mc.step4(env, src, SEG_NO_END, sid, ps, thrmax, lut);
             if (x == 1) fl = SEG_CUT;
             src.fill();  // step4 (SelFifo::top4) needs two held draws
         }
         if (fl) {
             mc.flush_stale(env, sid);
+            SegRec<M> r;
             r.b = src.idx - 1u;
             r.flags = fl;
             r.h = mc.h;
             r.w = mc.w;
             r.kb = mc.k;
-            r.dFh = mc.F;
-            r.span = (uint64_t)(mc.T - T0);
+            r.dFh = mc.F - Fq;  // since the sub's last checkpoint, like the counters and the span
+            r.span = (uint64_t)(mc.T - Tq);
+            r.qn = emitq.n();
 #pragma unroll
             for (int j = 0; j < SegRec<M>::NP; ++j) r.pend[j] = mc.pend[j];
             seg_snapshot<M>(r, src);
@@ -178,49 +237,66 @@ MSIM_HD uint32_t seg_work(Env &env, Src &src, uint32_t e, uint32_t sid, int64_t 
             if (!emit(r)) return SERR_CAP;
             if (fl == SEG_END) return 0;
             mc.begin(src);  // the quiet restart after the cut (pending find b + 1)
-            T0 = mc.T;
+            Tq = mc.T;
+            Fq = 0;
+            qleft = SEG_QWIN;
+            qnext = 0xFFFFFFFFu;
+            qon = true;
         }
     }
 }
 
-// ST lane state: the run's true settled state X (absolute time, real D) and the worker's replayed trajectory W
-// (D = infinity, restarted exactly where the worker restarted), each with its own draw source.
+// ST lane state: the run's true settled state X (absolute time, real D) and where it stands among the workers'
+// records: segment seg, the sub record q that ends X's current stretch (the first with b >= X's pending block),
+// the checkpoint cursor qi (the first checkpoint of seg after X's last join test).
 enum : uint32_t { ST_JUMP = 0, ST_WALK = 1, ST_ENGINE = 2, ST_END = 3, ST_DONE = 4 };
 template <int M>
 struct SegStitch {
-    SelMacro<M> X, W;
-    int64_t WT0;       // W.T at the start of its sub
-    uint32_t seg, q;   // W's sub (in JUMP: the sub to jump)
+    SelMacro<M> X;
+    uint32_t seg, q, qi;
+    uint32_t at_rec;     // JUMP: X joined the worker at sub q's end record (1) or at checkpoint qi - 1 (0)
     uint32_t mode;
-    uint32_t wnew;     // after the engine: W restarts from the cut record (seg, q - 1)
     uint32_t walk_back;  // after the engine: back to WALK (1) or END (0)
     uint32_t err;
 };
 
-// Rec access: const SegRec<M> &rec(seg, q) (or a copy), uint32_t count(seg), nseg.
-// EnvT: the true counters (C_F, C_S, C_A, C_B); EnvW: the replayed worker's (C_F, C_S only).
+// Recs: uint32_t count(seg); SegRec<M> rec(seg, q); void head(seg, q, b, flags); uint32_t qcount(seg);
+// uint32_t qc(seg, i) (a checkpoint's block); uint32_t qspan(seg, i); SegQRec<M> qrec(seg, i).
 // One action of a lane that is not in the engine; returns its new mode. ST_ENGINE: X needs the entity engine at
-// its pending find (the caller converts X with to_exact, steps the engine, and calls seg_after_engine).
-template <int M, class Recs, class EnvT, class EnvW, class Src>
-MSIM_HD uint32_t seg_stitch_step(SegStitch<M> &S, const Recs &R, EnvT &et, EnvW &ew, Src &st, Src &sw, int64_t D,
-                                 uint32_t sid, int64_t ps, int64_t thrmax, const uint32_t *lut)
+// its pending find (the caller converts X with to_exact, steps the engine, and takes X back; then mode =
+// walk_back ? ST_WALK : ST_END). ST_DONE with err == 0: the run ended in the settled form (the caller finishes X).
+// A run starts in ST_WALK at its first find (segment 0's worker starts quiet there: the first test joins).
+template <int M, class Recs, class EnvT, class Src>
+MSIM_HD uint32_t seg_stitch_step(SegStitch<M> &S, const Recs &R, EnvT &et, Src &st, int64_t D, uint32_t sid, int64_t ps,
+                                 int64_t thrmax, const uint32_t *lut)
 {
-    if (S.mode == ST_JUMP) {
-        if (S.q >= R.count(S.seg)) {  // the worker ran out of records: only past the pre-generated blocks
-            S.err |= SERR_DRAWS;
-            return S.mode = ST_DONE;
-        }
+    if (S.mode == ST_JUMP) {  // X equals the worker at its pending block: take the rest of sub q from the records
         const SegRec<M> r = R.rec(S.seg, S.q);
-        const int64_t Tb = S.X.T + (int64_t)r.span - (S.W.T - S.WT0);
-        if (Tb + thrmax >= D) return S.mode = ST_END;  // the run ends in this sub: replay it with the real D
-#pragma unroll
-        for (int kk = 0; kk < M; ++kk) {
-            et.add(C_F, (uint32_t)kk, r.dF[kk] - ew.get(C_F, (uint32_t)kk));
-            et.add(C_S, (uint32_t)kk, r.dS[kk] - ew.get(C_S, (uint32_t)kk));
-            ew.set(C_F, (uint32_t)kk, 0u);
-            ew.set(C_S, (uint32_t)kk, 0u);
+        const uint32_t nq = R.qcount(S.seg);
+        const bool ar = S.at_rec != 0u;
+        int64_t Tb = S.X.T;
+        if (!ar) {
+            Tb += (int64_t)r.span;
+            for (uint32_t j = S.qi; j < nq && R.qc(S.seg, j) <= r.b; ++j) Tb += R.qspan(S.seg, j);
         }
-        S.X.F += r.dFh - S.W.F;
+        if (Tb + thrmax >= D) return S.mode = ST_END;  // the run ends in this sub: the true state alone, real D
+        if (!ar) {
+            for (; S.qi < nq && R.qc(S.seg, S.qi) <= r.b; ++S.qi) {
+                const SegQRec<M> qr = R.qrec(S.seg, S.qi);
+                S.X.F += qr.dFh;
+#pragma unroll
+                for (int kk = 0; kk < M; ++kk) {
+                    et.add(C_F, (uint32_t)kk, qr.dF[kk]);
+                    et.add(C_S, (uint32_t)kk, qr.dS[kk]);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < M; ++kk) {
+                et.add(C_F, (uint32_t)kk, r.dF[kk]);
+                et.add(C_S, (uint32_t)kk, r.dS[kk]);
+            }
+            S.X.F += r.dFh;
+        }
         S.X.Ff = S.X.F;
         S.X.h = r.h;
         S.X.w = r.w;
@@ -233,23 +309,21 @@ MSIM_HD uint32_t seg_stitch_step(SegStitch<M> &S, const Recs &R, EnvT &et, EnvW 
         S.X.T = Tb;
         S.X.k = r.kb;
         seg_resume<M>(st, r);
-        if (r.flags & SEG_CUT) {
+        if (r.flags & SEG_CUT) {  // the true state is the worker's: it needs the engine at b too
             S.q += 1u;
-            S.wnew = 1u;
+            S.qi = r.qn;  // the next sub's checkpoints
             S.walk_back = 1u;
             return S.mode = ST_ENGINE;
         }
         // segment end: the next segment's worker started quiet at b
         S.seg += 1u;
         S.q = 0u;
-        seg_set_quiet<M>(S.W, r.kb, 0);
-        S.WT0 = 0;
-        if (seg_quiet<M>(S.X)) return S.mode = ST_JUMP;
-        seg_resume<M>(sw, r);
+        S.qi = 0u;
         return S.mode = ST_WALK;
     }
     if (S.mode == ST_END) {  // the true state alone, to the end of the run
         const int x = S.X.step4(et, st, D, sid, ps, thrmax, lut);
+        st.fill();
         if (x == 2) return S.mode = ST_DONE;
         if (x == 1) {
             S.walk_back = 0u;
@@ -257,52 +331,44 @@ MSIM_HD uint32_t seg_stitch_step(SegStitch<M> &S, const Recs &R, EnvT &et, EnvW 
         }
         return S.mode;
     }
-    // ST_WALK: W catches up with X one find at a time; at the same pending block, equal states coalesce
-    const uint32_t it = st.idx - 1u, iw = sw.idx - 1u;
-    if (iw < it) {
-        if (S.q >= R.count(S.seg)) {
+    // ST_WALK: the true state alone, one find at a time, until it meets the worker in the same state at the same
+    // block: at a quiet checkpoint, or at a sub's end record
+    const uint32_t i = st.idx - 1u;
+    uint32_t b = 0, fl = 0;
+    for (;;) {  // the record that ends X's stretch: the first with b >= i
+        if (S.q >= R.count(S.seg)) {  // past the pre-generated segments
             S.err |= SERR_DRAWS;
             return S.mode = ST_DONE;
         }
-        const SegRec<M> r = R.rec(S.seg, S.q);
-        if (iw > r.b) {  // cannot happen: the replay left the worker's path
-            S.err |= SERR_CAP;
-            return S.mode = ST_DONE;
-        }
-        if ((r.flags & SEG_END) && iw == r.b) {  // W reached its segment's end: the next worker starts quiet
-            seg_set_quiet<M>(S.W, S.W.k, S.W.T);
-            S.WT0 = S.W.T;
-#pragma unroll
-            for (int kk = 0; kk < M; ++kk) {
-                ew.set(C_F, (uint32_t)kk, 0u);
-                ew.set(C_S, (uint32_t)kk, 0u);
-            }
+        R.head(S.seg, S.q, b, fl);
+        if (b >= i) break;
+        if (fl & SEG_END) {  // X passed the segment's end: the next segment
             S.seg += 1u;
             S.q = 0u;
-            return S.mode;
-        }
-        const int x = S.W.step1(ew, sw, SEG_NO_END, sid, ps);
-        sw.fill();
-        if (x == 1) {  // the worker's cut: it restarted quiet at the next block
-            if (!(r.flags & SEG_CUT) || r.b != iw) {
-                S.err |= SERR_CAP;
-                return S.mode = ST_DONE;
-            }
+            S.qi = 0u;
+        } else {
             S.q += 1u;
-            S.W.begin(sw);
-            S.WT0 = S.W.T;
-#pragma unroll
-            for (int kk = 0; kk < M; ++kk) {
-                ew.set(C_F, (uint32_t)kk, 0u);
-                ew.set(C_S, (uint32_t)kk, 0u);
-            }
         }
-        return S.mode;
     }
-    if (iw == it && seg_same<M>(S.X, S.W)) {  // coalesced: the sub's remaining deltas are the true ones
+    const uint32_t nq = R.qcount(S.seg);
+    uint32_t c = 0xFFFFFFFFu;
+    while (S.qi < nq && (c = R.qc(S.seg, S.qi)) < i) ++S.qi;
+    if (S.qi < nq && c == i && seg_quiet<M>(S.X)) {  // both quiet at block i
+        ++S.qi;
         S.X.flush_stale(et, sid);
-        S.W.flush_stale(ew, sid);
+        S.at_rec = 0u;
         return S.mode = ST_JUMP;
+    }
+    if (b == i) {
+        const SegRec<M> r = R.rec(S.seg, S.q);
+        bool eq = (r.h == S.X.h) & (r.w == S.X.w);
+#pragma unroll
+        for (int j = 0; j < SegRec<M>::NP; ++j) eq &= r.pend[j] == S.X.pend[j];
+        if (eq) {
+            S.X.flush_stale(et, sid);
+            S.at_rec = 1u;
+            return S.mode = ST_JUMP;
+        }
     }
     const int x = S.X.step1(et, st, D, sid, ps);
     st.fill();  // a later step4 (END) needs two held draws
@@ -312,26 +378,6 @@ MSIM_HD uint32_t seg_stitch_step(SegStitch<M> &S, const Recs &R, EnvT &et, EnvW 
         return S.mode = ST_ENGINE;
     }
     return S.mode;
-}
-
-// After the engine handed X back settled (take_back succeeded and X.T < D): W restarts from the cut record if
-// the episode started at a cut; back to WALK or END.
-template <int M, class Recs, class EnvW, class Src>
-MSIM_HD void seg_after_engine(SegStitch<M> &S, const Recs &R, EnvW &ew, Src &sw)
-{
-    if (S.wnew) {
-        const SegRec<M> r = R.rec(S.seg, S.q - 1u);
-        seg_resume<M>(sw, r);
-        S.W.begin(sw);
-        S.WT0 = S.W.T;
-#pragma unroll
-        for (int kk = 0; kk < M; ++kk) {
-            ew.set(C_F, (uint32_t)kk, 0u);
-            ew.set(C_S, (uint32_t)kk, 0u);
-        }
-        S.wnew = 0u;
-    }
-    S.mode = S.walk_back ? ST_WALK : ST_END;
 }
 
 }  // namespace msim

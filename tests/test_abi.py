@@ -61,8 +61,7 @@ def test_config_validation_without_gpu(msim_lib_path):
                       ([Miner(k, 25, 1000, k < 4) for k in range(4)], 100),
                       ([Miner(0, 7, 1000, True), Miner(1, 3, 1000)], 10)):
         sim = Simulation(miners, total_weight=W)
-        # (one selfish miner, rare forks, a year: the segment-parallel form of E1, msim_selseg.h)
-        assert not sim.wide and sim.pipeline_info(1024)["uses_pipeline"] in (3, 6)
+        assert not sim.wide and sim.pipeline_info(1024)["uses_pipeline"] == 3
     # every other network with selfish miners runs on the general engine (msim_general.h): more than
     # MSIM_MAX_SELFISH selfish miners, or selfish miners in networks of more than 15 miners, any W
     for miners, W in (([Miner(k, 20, 1000, True) for k in range(5)], 100),
@@ -82,20 +81,20 @@ def test_config_validation_without_gpu(msim_lib_path):
                      total_weight=102400)
     assert big.pipeline_info(1024)["uses_pipeline"] == 4
     assert big.workspace_bytes(65536) < 3 * 2**30, big.workspace_bytes(65536)
-    # configs[2] at its per-GPU size: the segment-parallel form (msim_selseg.h) keeps every run's worker subs
-    # (~70 KB per run-year, ~9 GB of the 288 GB); E1 alone (MSIM_NO_SELSEG) stays under 1 GiB
+    # configs[2] at its per-GPU size: E1 stays under 1 GiB; the opt-in segment-parallel form (msim_selseg.h,
+    # MSIM_SELSEG) keeps every run's worker subs and checkpoints within its 24 GiB slice budget
     import os
-    c3 = Simulation(setup_miners(1000, selfish_perc=40))
-    info = c3.pipeline_info(131072)
-    assert info["uses_pipeline"] == 6 and info["segments"] >= 2, info
-    assert c3.workspace_bytes(131072) < 24 * 2**30, c3.workspace_bytes(131072)
-    os.environ["MSIM_NO_SELSEG"] = "1"
+    e1 = Simulation(setup_miners(1000, selfish_perc=40))
+    assert e1.pipeline_info(131072)["uses_pipeline"] == 3
+    assert e1.workspace_bytes(131072) < 2**30
+    os.environ["MSIM_SELSEG"] = "1"
     try:
-        e1 = Simulation(setup_miners(1000, selfish_perc=40))
-        assert e1.pipeline_info(131072)["uses_pipeline"] == 3
-        assert e1.workspace_bytes(131072) < 2**30
+        c3 = Simulation(setup_miners(1000, selfish_perc=40))
+        info = c3.pipeline_info(131072)
+        assert info["uses_pipeline"] == 6 and info["segments"] >= 2, info
+        assert c3.workspace_bytes(131072) < 26 * 2**30, c3.workspace_bytes(131072)
     finally:
-        del os.environ["MSIM_NO_SELSEG"]
+        del os.environ["MSIM_SELSEG"]
     # the large-network path (msim_wide.h): more than 15 honest miners, or integer weights
     assert Simulation([Miner(k, 7 if k < 10 else 5, 1000) for k in range(16)]).wide
     assert not Simulation(setup_miners()).wide

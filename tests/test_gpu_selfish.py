@@ -30,7 +30,7 @@ def msim(msim_lib_path):
 def _run(msim, p, q, s, n, begin=0, seed=1000, duration=D, W=100):
     miners = [msim.Miner(k, p[k], q[k], bool(s[k])) for k in range(len(p))]
     sim = msim.Simulation(miners, duration, total_weight=W)
-    assert sim.pipeline_info(n)["uses_pipeline"] in (3, 6)  # E1, or its segment-parallel form (msim_selseg.h)
+    assert sim.pipeline_info(n)["uses_pipeline"] == 3  # E1 (its segment-parallel form is opt-in: test_gpu_selseg.py)
     return sim.run(n, begin, seed, 0, per_run=True)
 
 

@@ -1,6 +1,6 @@
 """The segment-parallel form of E1 on the GPU (msim_selseg.h: SW settled-form workers per (run, segment), ST stitching
-each run with the entity engine), through the C ABI: run by run against the oracle, and against E1 itself
-(MSIM_NO_SELSEG) at sizes the oracle cannot follow. The reference behaviour is RunSimulation (main.cpp:128-192) with
+each run with the entity engine; opt-in, MSIM_SELSEG=1), through the C ABI: run by run against the oracle, and
+against E1 itself (the default) at sizes the oracle cannot follow. The reference behaviour is RunSimulation (main.cpp:128-192) with
 one selfish miner (simulation.h:55, 62-180); BASELINE configs[2]. MSIM_SEG_NSEG forces many short segments so that
 every segment boundary's coalescence walk runs many times per run."""
 import random
@@ -12,6 +12,11 @@ pytestmark = pytest.mark.gpu
 
 YEAR = 31_556_952_000
 C3 = ([40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [1] + [0] * 8)
+
+
+@pytest.fixture(autouse=True)
+def _selseg(monkeypatch):
+    monkeypatch.setenv("MSIM_SELSEG", "1")
 
 
 @pytest.fixture(scope="module")
@@ -57,23 +62,23 @@ def test_gpu_selseg_c3_vs_oracle(msim, oracle, monkeypatch, nseg):
 
 
 def test_gpu_selseg_equals_e1(msim, monkeypatch):
-    """32 768 configs[2] runs: SW + ST and E1 (MSIM_NO_SELSEG) agree per run and in the fixed-point sums."""
+    """32 768 configs[2] runs: SW + ST and E1 (the default) agree per run and in the fixed-point sums."""
     a = _sim(msim, *C3).run(32768, 7000, 1000, 0, per_run=True)
-    monkeypatch.setenv("MSIM_NO_SELSEG", "1")
+    monkeypatch.delenv("MSIM_SELSEG")
     sim = _sim(msim, *C3)
     assert sim.pipeline_info(32768)["uses_pipeline"] == 3
     b = sim.run(32768, 7000, 1000, 0, per_run=True)
     _same(a, b)
 
 
-@pytest.mark.parametrize("h,prop", [(10, 100), (25, 500), (33, 2000), (49, 250), (45, 1000)])
+@pytest.mark.parametrize("h,prop", [(10, 100), (25, 500), (33, 1000), (49, 250), (45, 1500)])
 def test_gpu_selseg_grid_points_vs_e1(msim, monkeypatch, h, prop):
     """Points of the configs[3] grid the segment-parallel form serves (rare cuts), 4 096 runs x 1 year, against E1."""
     p, q, s = [h, 59 - h, 12, 11, 8, 5, 3, 1, 1], [prop] * 9, [1] + [0] * 8
     sim = _sim(msim, p, q, s)
     assert sim.pipeline_info(4096)["uses_pipeline"] == 6
     a = sim.run(4096, 0, 1000, 0, per_run=True)
-    monkeypatch.setenv("MSIM_NO_SELSEG", "1")
+    monkeypatch.delenv("MSIM_SELSEG")
     b = _sim(msim, p, q, s).run(4096, 0, 1000, 0, per_run=True)
     _same(a, b)
 

@@ -24,6 +24,7 @@ def seg(native_tests):
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
     lib.selseg_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    lib.selseg_qcap.argtypes = [ctypes.c_uint32]
 
     def run(weights, props, selfish, duration, si, sp, nseg, cap=1 << 20, W=100):
         m = len(weights)
@@ -40,11 +41,13 @@ def seg(native_tests):
         return rc, np.array([[f[k], s[k]] for k in range(m)], dtype=np.int64), bh.value
 
     def stats():
-        out = (ctypes.c_uint64 * 6)()
+        out = (ctypes.c_uint64 * 7)()
         lib.selseg_stats(out)
-        return dict(zip(("subs", "cuts", "jumps", "walk_steps", "engine_entries", "end_steps"), list(out)))
+        return dict(zip(("subs", "cuts", "jumps", "walk_steps", "engine_entries", "end_steps", "checkpoints"),
+                        list(out)))
 
     run.stats = stats
+    run.qcap = lib.selseg_qcap
     return run
 
 
@@ -101,3 +104,19 @@ def test_overflow_is_reported(seg):
     w, p, s = [40, 19, 12, 11, 8, 5, 3, 1, 1], [30000] * 9, [1] + [0] * 8
     rc, _, _ = seg(w, p, s, D // 12, 5, 6, 2, cap=4)
     assert rc == 1
+
+
+@pytest.mark.parametrize("qcap", [0 + 1, 7, 40])
+def test_checkpoint_room_runs_out(seg, oracle, qcap):
+    """Workers whose checkpoint room fills up store no more checkpoints (the device's seg_qcap bound): the stitch
+    walks further and the run is still the oracle's."""
+    w, p, s = [40, 19, 12, 11, 8, 5, 3, 1, 1], [1000] * 9, [1] + [0] * 8
+    seg.qcap(qcap)
+    try:
+        seg.stats()
+        for nseg in (1, 4):
+            _check(seg, oracle, w, p, s, D // 6, 31 + qcap, nseg)
+        st = seg.stats()
+        assert st["checkpoints"] <= 4 * qcap + qcap, st
+    finally:
+        seg.qcap(0)
