@@ -67,7 +67,8 @@ struct DevCtx {
         for (uint32_t i = lane; i < lleft; i += 64u)
             if (lo + i < a.lcap) a.list[lo + i].run = EP_HOLE;
     }
-    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
+    __device__ void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp,
+                         uint32_t skip)
     {
         const uint64_t mask = __builtin_amdgcn_ballot_w64(s) & amask;
         // rank of this lane among the slow ones (asm volatile: computed here, not hoisted out of the loop)
@@ -99,7 +100,8 @@ struct DevCtx {
             e.offset = offset;
             e.w0 = w0;
             e.w1 = w1;
-            e.pad[0] = e.pad[1] = 0;
+            e.skip = skip;
+            e.pad = 0;
             e.ri = ri;
             e.rp = rp;
             a.list[idx] = e;

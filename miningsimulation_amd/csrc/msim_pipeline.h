@@ -59,8 +59,9 @@ struct EpEntry {
     uint32_t block;   // block index within the run
     uint64_t offset;  // T_block - (start time of its segment), ms
     uint32_t w0, w1;  // (interval << 5 | finder) of the block and of the next one
-    uint32_t pad[2];
-    Rng ri, rp;       // both streams, positioned at the block after w1
+    uint32_t skip;    // draws from ri / rp's position to the block after w1 (1-4)
+    uint32_t pad;
+    Rng ri, rp;       // both streams at the start of K1's quad of w1's block: `skip` draws before the block after w1
 };
 
 // A group of the band (where a run can end): the first block's word and both streams after it.
@@ -305,10 +306,11 @@ MSIM_HD void draw_quad_exact(Rng ri, Rng rp, const LogTab *__restrict__ lt, cons
 // One (run, segment) worker: SEG blocks from the jumped RNG states. Ctx supplies the side effects:
 //   count(info)                       per-owner counter of this lane (+1 for owner info_finder(info))
 //   vote(s)                           nonzero when s holds for some active lane of the wave (host: s)
-//   slow(s, block, offset, w0, w1, ri, rp)
+//   slow(s, block, offset, w0, w1, ri, rp, skip)
 //                                     called after a nonzero vote: records a non-fast block when s
 //                                     (offset = its find time minus the segment's start; its word, the
-//                                     next one and both streams after them; the finder's threshold)
+//                                     next one; both streams at the quad's start, `skip` draws before the
+//                                     block after the next one: the consumer steps them, not the wave)
 //   group(g, sum, end)                band only: sum of the group's intervals, and the time from the segment's
 //                                     start to the group's end
 //   quad()                            start of a quad of blocks
@@ -360,15 +362,9 @@ MSIM_HD uint64_t draw_segment(Ctx &cx, Rng &ri, Rng &rp, const LogTab *__restric
                 gacc += Icur;
                 const bool slow = I[q] <= info_fthr(infocur);  // I_{i+1} vs the finder's delay
                 cx.count(infocur);
-                if (cx.vote(slow)) {
-                    Rng a = ri0, b = rp0;  // the streams after block i+1
-                    for (int t = 0; t <= q; ++t) {
-                        rng_next(a);
-                        rng_next(b);
-                    }
+                if (cx.vote(slow))  // the streams after block i+1 are the quad's start + q + 1 draws (K2 steps them)
                     cx.slow(slow, b0 + g * GROUP + q4 * K1_QB + (uint32_t)q, tsum + gacc, (Icur << 5) | info_finder(infocur),
-                            (I[q] << 5) | info_finder(info[q]), a, b);
-                }
+                            (I[q] << 5) | info_finder(info[q]), ri0, rp0, (uint32_t)q + 1u);
                 Icur = I[q];
                 infocur = info[q];
             }
@@ -792,6 +788,10 @@ MSIM_HD void episode_entry(const SimParams &p, const PipeArgs &a, uint32_t idx)
     src.pt = a.tab.pick;
     src.ri = e.ri;
     src.rp = e.rp;
+    for (uint32_t t = 0; t < e.skip; ++t) {  // K1 stored its quad's start states (EpEntry::skip)
+        rng_next(src.ri);
+        rng_next(src.rp);
+    }
     src.nb = a.nb;
     src.index = e.block;
     src.cur = e.w0;

@@ -31,11 +31,11 @@ struct HostCtx {
     }
     bool vote(bool s) const { return s; }
     void quad() {}
-    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp)
+    void slow(bool s, uint32_t block, uint64_t offset, uint32_t w0, uint32_t w1, const Rng &ri, const Rng &rp, uint32_t skip)
     {
         if (!s) return;
         const uint32_t idx = (uint32_t)list->size();
-        if (idx < L.lcap) list->push_back(EpEntry{r, block, offset, w0, w1, {0, 0}, ri, rp});
+        if (idx < L.lcap) list->push_back(EpEntry{r, block, offset, w0, w1, skip, 0, ri, rp});
         if (nsl < L.cap) (*slots)[((size_t)seg * L.cap + nsl) * L.nr + r] = idx;
         ++nsl;
     }
