@@ -1,3 +1,4 @@
+import fcntl
 import os
 import subprocess
 import sys
@@ -50,8 +51,12 @@ def native_tests():
     kat = os.path.join(ROOT, "build", "libselkat_host.so")
     seg = os.path.join(ROOT, "build", "libselseg_host.so")
     outs = (lib, chk, pipe, wide, sel, gen, kat, seg)
-    if not all(os.path.exists(p) for p in outs) or _stale(outs):
-        ge.build_native_tests()
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    # one builder at a time (pytest-xdist workers share build/): the others wait, then find the outputs fresh
+    with open(os.path.join(ROOT, "build", ".native_tests.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not all(os.path.exists(p) for p in outs) or _stale(outs):
+            ge.build_native_tests()
     return {"model_host": lib, "draws_check": chk, "pipeline_host": pipe, "wide_host": wide, "sel_host": sel,
             "general_host": gen, "selkat_host": kat, "selseg_host": seg}
 
