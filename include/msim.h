@@ -98,6 +98,12 @@ int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t du
 /* 1 when the config runs on the large-network pipeline (set MSIM_FORCE_WIDE=1 in the environment before
  * msim_config_create to route small honest networks there too, e.g. for cross-path parity checks). */
 int msim_config_is_wide(const msim_config *cfg);
+/* How many launches of this config the caller keeps in flight at once (default 1; e.g. 2 when steps
+ * alternate over two HIP streams). The event-skipping pipeline plans its draw kernel's grid for it: two
+ * rounds of resident waves for one launch, one round each for two. A tuning hint with no effect on results;
+ * it changes msim_workspace_bytes, so set it before sizing the workspace. MSIM_E_INVALID outside 1..64.
+ * (No reference counterpart: the reference runs one std::async batch at a time, main.cpp:205-220.) */
+int msim_config_set_concurrent_launches(msim_config *cfg, uint32_t n);
 void msim_config_destroy(msim_config *cfg);
 uint32_t msim_config_miner_count(const msim_config *cfg);
 

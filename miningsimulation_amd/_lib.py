@@ -28,6 +28,7 @@ EXPORTED = (
     "msim_config_create",
     "msim_config_create_weighted",
     "msim_config_is_wide",
+    "msim_config_set_concurrent_launches",
     "msim_config_destroy",
     "msim_config_miner_count",
     "msim_run",
@@ -131,6 +132,8 @@ def _load() -> ctypes.CDLL:
     lib.msim_config_create_weighted.restype = ctypes.c_int
     lib.msim_config_is_wide.argtypes = [vp]
     lib.msim_config_is_wide.restype = ctypes.c_int
+    lib.msim_config_set_concurrent_launches.argtypes = [vp, u32]
+    lib.msim_config_set_concurrent_launches.restype = ctypes.c_int
     lib.msim_config_destroy.argtypes = [vp]
     lib.msim_config_destroy.restype = None
     lib.msim_config_miner_count.argtypes = [vp]

@@ -61,6 +61,7 @@ struct msim_config {
     uint8_t self[MSIM_MAX_MINERS];
     double rho;      // probability that a block is not "fast" (msim_pipeline.h)
     bool pipe_ok;    // event-skipping pipeline eligible (honest network, rare forks)
+    uint32_t jobs = 1;  // launches the caller keeps in flight at once (msim_config_set_concurrent_launches)
     std::mutex mu;
     struct Tab {
         int dev;
@@ -180,9 +181,16 @@ uint32_t draw_slots()
     return (uint32_t)(cus * blocks * 4);
 }
 
+// K1's grid is planned for the launches in flight: one launch gets two rounds of resident waves (more, shorter
+// segments: the second round fills the first one's ragged end), two launches on two streams one round each
+// (the other launch fills it). Measured on MI355X, c2 (profiles/r06/k1slots/): one launch 3.31 -> 3.14 ms per
+// step with two rounds; two streams 2.82 ms per step with one round each against 2.89 with two.
 msim::PipeLayout pipe_layout(const msim_config *c, uint64_t n_runs)
 {
-    return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET, draw_slots());
+    const uint32_t jobs = c->jobs ? c->jobs : 1u;
+    uint32_t slots = draw_slots() * 2u / jobs;
+    if (slots < 1u) slots = 1u;
+    return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET, slots);
 }
 
 // Pipeline tables for this config on the current device: pick table, log table, jump matrices for
@@ -915,6 +923,14 @@ int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t du
 }
 
 int msim_config_is_wide(const msim_config *cfg) { return cfg && cfg->wide ? 1 : 0; }
+
+int msim_config_set_concurrent_launches(msim_config *cfg, uint32_t n)
+{
+    if (!cfg || n < 1 || n > 64) return MSIM_E_INVALID;
+    std::lock_guard<std::mutex> g(cfg->mu);
+    cfg->jobs = n;
+    return MSIM_OK;
+}
 
 void msim_config_destroy(msim_config *cfg)
 {

@@ -140,6 +140,12 @@ class Simulation:
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
+    def set_concurrent_launches(self, n: int) -> None:
+        """msim_config_set_concurrent_launches: how many launches of this config the caller keeps in flight
+        (e.g. steps alternating over n HIP streams). A grid-planning hint, no effect on results; it changes
+        workspace_bytes, so call it before sizing the workspace."""
+        check(lib.msim_config_set_concurrent_launches(self._h, int(n)), "msim_config_set_concurrent_launches")
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:

@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -115,6 +117,20 @@ def test_config_validation_without_gpu(msim_lib_path):
             assert e.code == code, (W, e)
         else:
             raise AssertionError(f"accepted invalid weighted network (W={W})")
+
+
+def test_concurrent_launches_hint(msim_lib_path):
+    """msim_config_set_concurrent_launches: 1..64 accepted, anything else MSIM_E_INVALID; it may change the
+    workspace the pipeline asks for (K1's grid), never the config's validity."""
+    from miningsimulation_amd import MsimError, Simulation, setup_miners
+
+    sim = Simulation(setup_miners(100))
+    for bad in (0, 65):
+        with pytest.raises(MsimError):
+            sim.set_concurrent_launches(bad)
+    for ok in (1, 2, 64):
+        sim.set_concurrent_launches(ok)
+        assert sim.workspace_bytes(32768) > 0
 
 
 def test_report_format():

@@ -381,3 +381,32 @@ def test_gpu_dirty_workspace_equals_clean(msim, preset):
         assert torch.equal(a, b)
     for a, b in zip(out[0], out[2]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("preset", ["c1", "c2"])
+def test_gpu_concurrent_launch_plans_agree(msim, preset):
+    """msim_config_set_concurrent_launches only re-plans K1's grid (two rounds of shorter segments for one launch
+    in flight, one round for two): every run's counters and the sums are the same for 1, 2 and 4."""
+    import torch
+
+    n = 8192
+    dev = torch.device("cuda", 0)
+    out = []
+    for jobs in (1, 2, 4):
+        sim = msim.Simulation(msim.PRESETS[preset]())
+        sim.set_concurrent_launches(jobs)
+        m = len(sim.miners)
+        ws = torch.empty((sim.workspace_bytes(n),), dtype=torch.uint8, device=dev)
+        sums = torch.zeros((m, 6), dtype=torch.int64, device=dev)
+        status = torch.zeros(2, dtype=torch.int32, device=dev)
+        rec = torch.zeros((n, m, 2), dtype=torch.int32, device=dev)
+        bh = torch.zeros(n, dtype=torch.int32, device=dev)
+        sim.launch(n, 4096, 1000, sums, ws, status, d_per_run=rec, d_best_height=bh)
+        torch.cuda.synchronize()
+        assert int(status[1]) == 0
+        out.append((sim.pipeline_info(n)["segments"], sums.cpu(), rec.cpu(), bh.cpu()))
+        del ws
+    assert out[0][0] > out[1][0], [o[0] for o in out]  # one launch in flight: more, shorter segments
+    for o in out[1:]:
+        for a, b in zip(out[0][1:], o[1:]):
+            assert torch.equal(a, b)
