@@ -23,6 +23,10 @@ __device__ void sel_engprof_acc(int i, uint64_t c)
 }
 #endif
 
+#ifndef SEL_SRC_LDS
+#define SEL_SRC_LDS 1  // E1's draw source parked in LDS during engine phases (SelLdsSrc); 0: in registers (A/B)
+#endif
+
 #ifndef SEL_WAVES
 #define SEL_WAVES 2  // E1 occupancy target (waves per SIMD): 256 VGPRs, no spills
 #endif
@@ -134,6 +138,65 @@ struct SelFastDraw {
     }
 };
 
+// E1's draw source during an engine phase: the lane's held draws and both RNG states wait in its LDS column
+// (p[i * TPB], SEL_SRC_WORDS words) instead of registers, so that the engine step, which needs every register
+// it can get, does not carry them (measured: its loop spilled 24 scratch instructions per iteration, the bulk of
+// E1's 37 GB of HBM traffic per configs[2] launch). The engine takes a draw per find (next); the rest of the
+// draw state (tables, constants) is wave-uniform.
+constexpr int SEL_SRC_WORDS = 17;  // ri, rp (8), I0..I3, k0..k3 (8), n
+template <int M>
+struct SelLdsSrc {
+    uint32_t *p;        // &s_src[0][tid]
+    SelFastDraw<M> d;   // tables and constants (ri / rp are loaded from the column for each fresh draw)
+    __device__ __forceinline__ uint32_t &w(int i) { return p[i * TPB]; }
+    template <class F>
+    __device__ __forceinline__ void park(const F &f)
+    {
+        w(0) = (uint32_t)f.d.ri.s0; w(1) = (uint32_t)(f.d.ri.s0 >> 32);
+        w(2) = (uint32_t)f.d.ri.s1; w(3) = (uint32_t)(f.d.ri.s1 >> 32);
+        w(4) = (uint32_t)f.d.rp.s0; w(5) = (uint32_t)(f.d.rp.s0 >> 32);
+        w(6) = (uint32_t)f.d.rp.s1; w(7) = (uint32_t)(f.d.rp.s1 >> 32);
+        w(8) = f.I0; w(9) = f.I1; w(10) = f.I2; w(11) = f.I3;
+        w(12) = f.k0; w(13) = f.k1; w(14) = f.k2; w(15) = f.k3;
+        w(16) = f.n;
+    }
+    template <class F>
+    __device__ __forceinline__ void unpark(F &f)
+    {
+        f.d.ri.s0 = ((uint64_t)w(1) << 32) | w(0);
+        f.d.ri.s1 = ((uint64_t)w(3) << 32) | w(2);
+        f.d.rp.s0 = ((uint64_t)w(5) << 32) | w(4);
+        f.d.rp.s1 = ((uint64_t)w(7) << 32) | w(6);
+        f.I0 = w(8); f.I1 = w(9); f.I2 = w(10); f.I3 = w(11);
+        f.k0 = w(12); f.k1 = w(13); f.k2 = w(14); f.k3 = w(15);
+        f.n = w(16);
+    }
+    __device__ __forceinline__ bool next(uint32_t &I, uint32_t &k)
+    {
+        const uint32_t n = w(16);
+        if (n == 0u) {  // a fresh draw from the parked streams
+            d.ri.s0 = ((uint64_t)w(1) << 32) | w(0);
+            d.ri.s1 = ((uint64_t)w(3) << 32) | w(2);
+            d.rp.s0 = ((uint64_t)w(5) << 32) | w(4);
+            d.rp.s1 = ((uint64_t)w(7) << 32) | w(6);
+            d.draw(I, k);
+            w(0) = (uint32_t)d.ri.s0; w(1) = (uint32_t)(d.ri.s0 >> 32);
+            w(2) = (uint32_t)d.ri.s1; w(3) = (uint32_t)(d.ri.s1 >> 32);
+            w(4) = (uint32_t)d.rp.s0; w(5) = (uint32_t)(d.rp.s0 >> 32);
+            w(6) = (uint32_t)d.rp.s1; w(7) = (uint32_t)(d.rp.s1 >> 32);
+            return true;
+        }
+        I = w(8);  // the oldest held draw, then the FIFO shifts
+        k = w(12);
+        w(8) = w(9); w(9) = w(10); w(10) = w(11);
+        w(12) = w(13); w(13) = w(14); w(14) = w(15);
+        w(16) = n - 1u;
+        return true;
+    }
+    __device__ __forceinline__ void prefetch() {}
+    __device__ __forceinline__ void settle() {}
+};
+
 template <int M>
 __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 {
@@ -181,8 +244,10 @@ __device__ __forceinline__ void sel_terms(const SelOut &o, uint64_t (&v)[6 * M])
 #endif
 template <int M, class SelT, class Env, class Src>
 __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P, int64_t D, SelOut &o, uint32_t *mcs,
-                                          const uint32_t *lut)
+                                          const uint32_t *lut, uint32_t *srcs = nullptr)
 {
+    // E1's draw source waits in LDS during engine phases (SelLdsSrc); E2 keeps it in registers
+    constexpr bool lds_src = SEL_SRC_LDS && std::is_same_v<Src, SelFifo<SelFastDraw<M>>>;
     SelMacro<M> mc;
     // A lane that finishes parks its counters in its own LDS counter rows (C_F, C_S) so that no result
     // register stays live across the loop of the others.
@@ -241,10 +306,19 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
 #if SEL_MC_LDS
             mc.save(mcs, TPB);  // saved and reloaded for every lane: no settled-form register is live here
 #endif
+            [[maybe_unused]] std::conditional_t<lds_src, SelLdsSrc<M>, char> ls{};
+            if constexpr (lds_src) {
+                ls.p = srcs;
+                ls.d = src.d;
+                ls.park(src);
+            }
+            uint32_t refill = 0;  // lanes back in the settled form: top the FIFO up after the phase
             for (;;) {
                 if (mode == 2) {
                     src.prefetch();
-                    const bool live = s.step(env, src, D);
+                    bool live;
+                    if constexpr (lds_src) live = s.step(env, ls, D);
+                    else live = s.step(env, src, D);
                     src.settle();
                     if (!live) {
                         SelOut r;
@@ -260,7 +334,8 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
                                 park(r);
                                 mode = 3;
                             } else {
-                                src.fill();  // the settled form starts every step with two held draws
+                                if constexpr (lds_src) refill = 1u;
+                                else src.fill();  // the settled form starts every step with two held draws
 #if SEL_MC_LDS
                                 tb.save(mcs, TPB);
 #else
@@ -276,6 +351,10 @@ __device__ __forceinline__ void sel_mixed(Env &env, Src &src, const SelParams *P
                 pl_e += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == 2));
 #endif
                 if (__builtin_amdgcn_ballot_w64(mode == 2) == 0ull) break;
+            }
+            if constexpr (lds_src) {
+                ls.unpark(src);
+                if (refill) src.fill();  // the settled form starts every step with two held draws
             }
 #if SEL_MC_LDS
             mc.load(mcs, TPB);
@@ -351,6 +430,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
 {
     __shared__ uint32_t s_cnt[4 * M][TPB];
     __shared__ uint32_t s_mc[NS == 1 && SEL_MC_LDS ? SelMacro<M>::NW : 1][TPB];
+    __shared__ uint32_t s_src[NS == 1 && SEL_SRC_LDS ? SEL_SRC_WORDS : 1][TPB];  // SelLdsSrc columns
     __shared__ uint32_t s_tab[SP_LUT];  // four-find transitions (msim_selm.h sp_lut_entry)
     __shared__ int64_t s_prop[MAXM];
     __shared__ uint8_t s_lut[128];
@@ -394,7 +474,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(SEL_WAVES, 
         if (a.force_retry) {
             o.err = SERR_CAP;
         } else if constexpr (NS == 1) {
-            sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid], s_tab);
+            sel_mixed<M, Sel<M, NS, NA, NG, NQ, NC>>(env, src, P, D, o, &s_mc[0][tid], s_tab, &s_src[0][tid]);
         } else {  // several selfish miners: the engine alone
             Sel<M, NS, NA, NG, NQ, NC> s;
             s.init(P->m, P->sids);
