@@ -473,6 +473,13 @@ SelCfgWs sel_cfg_layout(const msim_config *cfg, uint64_t n_runs)
     return c;
 }
 
+#ifndef MSIM_XTH_MID
+#define MSIM_XTH_MID 32  // engine-phase threshold for delays of 2-10 s (build_sel_params)
+#endif
+#ifndef MSIM_XTH_HI
+#define MSIM_XTH_HI 48  // and above 10 s
+#endif
+
 // One SelParams for a validated network (weights summing to W, <= MSIM_MAX_MINERS miners).
 void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms, uint64_t W, msim::SelParams *sp)
 {
@@ -504,7 +511,7 @@ void build_sel_params(const msim_miner *miners, uint32_t n, int64_t duration_ms,
     // configs[3] grid up to 30 s with 32; profiles/r02/xth_v.txt).
     int64_t pmax = 0;
     for (uint32_t k = 0; k < n; ++k) pmax = miners[k].propagation_ms > pmax ? miners[k].propagation_ms : pmax;
-    sp->xth = pmax <= 2000 ? 16u : (pmax <= 10000 ? 32u : 48u);
+    sp->xth = pmax <= 2000 ? 16u : (pmax <= 10000 ? (uint32_t)MSIM_XTH_MID : (uint32_t)MSIM_XTH_HI);
     if (const char *e = getenv("MSIM_SEL_XTH")) sp->xth = (uint32_t)atoi(e);  // A/B override
 }
 
