@@ -157,7 +157,7 @@ struct SegQRec {
 // Env: the worker's counter rows C_F / C_S (zero at entry), prop_tab. emit(rec) / emitq(qrec) store a sub's end
 // record / a quiet checkpoint and return false when the caller cannot hold it (a record: the run is then
 // recomputed by E2; a checkpoint: the sub stores no more);
-// nq() is the number of checkpoints stored so far (SegRec::qn). Inside a quiet window, and from a multiple of
+// emitq.n() is the number of checkpoints stored so far (SegRec::qn). Inside a quiet window, and from a multiple of
 // SEG_QEVERY to the next quiet block, the worker steps one find at a time (it must see every pending block);
 // elsewhere four. Returns 0 or an SERR_* code.
 template <int M, class Env, class Src, class Emit, class EmitQ>
