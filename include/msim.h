@@ -99,7 +99,7 @@ int msim_config_create_weighted(const msim_miner *miners, uint32_t n, int64_t du
  * msim_config_create to route small honest networks there too, e.g. for cross-path parity checks). */
 int msim_config_is_wide(const msim_config *cfg);
 /* How many launches of this config the caller keeps in flight at once (default 1; e.g. 2 when steps
- * alternate over two HIP streams). The event-skipping pipeline plans its draw kernel's grid for it: two
+ * alternate over two HIP streams). The event-skipping pipeline plans its draw kernel's grid for it: three
  * rounds of resident waves for one launch, one round each for two. A tuning hint with no effect on results;
  * it changes msim_workspace_bytes, so set it before sizing the workspace. MSIM_E_INVALID outside 1..64.
  * (No reference counterpart: the reference runs one std::async batch at a time, main.cpp:205-220.) */

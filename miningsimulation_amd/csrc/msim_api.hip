@@ -181,14 +181,15 @@ uint32_t draw_slots()
     return (uint32_t)(cus * blocks * 4);
 }
 
-// K1's grid is planned for the launches in flight: one launch gets two rounds of resident waves (more, shorter
-// segments: the second round fills the first one's ragged end), two launches on two streams one round each
-// (the other launch fills it). Measured on MI355X, c2 (profiles/r06/k1slots/): one launch 3.31 -> 3.14 ms per
-// step with two rounds; two streams 2.82 ms per step with one round each against 2.89 with two.
+// K1's grid is planned for the launches in flight: one launch gets three rounds of resident waves (more,
+// shorter segments: later rounds fill the earlier ones' ragged ends), two launches on two streams one round
+// each (the other launch fills it). Measured on MI355X, c2 serial (profiles/r06/k1slots/): 3.31 / 3.13 / 3.08 /
+// 3.21 / 3.21 ms per step with 1 / 2 / 3 / 5 / 6 rounds (more segments also cost K2 and K3); two streams 2.82 ms
+// per step with one round each against 2.89 with 1.5 and two.
 msim::PipeLayout pipe_layout(const msim_config *c, uint64_t n_runs)
 {
     const uint32_t jobs = c->jobs ? c->jobs : 1u;
-    uint32_t slots = draw_slots() * 2u / jobs;
+    uint32_t slots = jobs == 1u ? draw_slots() * 3u : draw_slots() * 2u / jobs;
     if (slots < 1u) slots = 1u;
     return msim::pipe_layout_for(c->rho, c->n, c->p.duration_ms, n_runs, PIPE_SLICE_BUDGET, slots);
 }

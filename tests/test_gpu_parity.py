@@ -385,7 +385,7 @@ def test_gpu_dirty_workspace_equals_clean(msim, preset):
 
 @pytest.mark.parametrize("preset", ["c1", "c2"])
 def test_gpu_concurrent_launch_plans_agree(msim, preset):
-    """msim_config_set_concurrent_launches only re-plans K1's grid (two rounds of shorter segments for one launch
+    """msim_config_set_concurrent_launches only re-plans K1's grid (three rounds of shorter segments for one launch
     in flight, one round for two): every run's counters and the sums are the same for 1, 2 and 4."""
     import torch
 
